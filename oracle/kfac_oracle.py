@@ -1,0 +1,205 @@
+"""CPU oracle: a numpy restatement of the reference's KFAC hot path.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in `bnn_kfac_amd/` imports this module; only
+`tests/`, `__graft_entry__.smoke()` and `bench.py`'s `cpu_baseline` leg may use
+it, and only as the checker (or the timed CPU baseline), never as the thing
+shipped.
+
+Parity status: PINNED.  Every function below is checked against golden vectors
+produced by running the real reference read-only in the build container
+(`tests/golden/make_goldens.py`, fixtures `tests/golden/*.npz`, checks in
+`tests/test_oracle_golden.py`).
+
+Each function can run in float32 (mirroring the reference's fp32 op sequence,
+rounding included as far as numpy allows) or float64 (the "truth" the GPU path's
+fp64 inversion is judged against).  Citations are `path:line` under
+`/root/reference/`.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+# --------------------------------------------------------------------------- factors
+def linear_factor_A(a: np.ndarray, has_bias: bool, dtype=np.float32) -> np.ndarray:
+    """First factor of a Linear layer for one batch.
+
+    models/curvatures.py:345-349: f = [a^T; 1^T] (d_in(+1) x B), A = f f^T / B.
+    """
+    f = np.asarray(a, dtype=dtype).T
+    if has_bias:
+        f = np.concatenate([f, np.ones((1, f.shape[1]), dtype=dtype)], axis=0)
+    return (f @ f.T) / dtype(f.shape[1])
+
+
+def grad_factor(g_rec: np.ndarray, dtype=np.float32) -> np.ndarray:
+    """Second factor for one batch of recorded output gradients.
+
+    models/curvatures.py:352-356.  Linear: b = g_rec^T (d_out x B).
+    Conv2d: b = g_rec.permute(1,0,2,3).view(C_out, B*L).  G = b b^T / cols.
+    `g_rec` is already `grad_output * B` (the backward hook, curvatures.py:322-323).
+    """
+    g = np.asarray(g_rec, dtype=dtype)
+    if g.ndim == 4:
+        b = np.transpose(g, (1, 0, 2, 3)).reshape(g.shape[1], -1)
+    else:
+        b = g.T
+    return (b @ b.T) / dtype(b.shape[1])
+
+
+def unfold(x: np.ndarray, kernel, padding, stride) -> np.ndarray:
+    """numpy restatement of `F.unfold(x, kernel, padding=, stride=)` (dilation 1).
+
+    Returns (B, C*kh*kw, L) with row index c*kh*kw + ki*kw + kj and
+    L = Ho*Wo in row-major (oh, ow) order, exactly torch's im2col order.
+    """
+    kh, kw = kernel
+    ph, pw = padding
+    sh, sw = stride
+    B, C, H, W = x.shape
+    xp = np.zeros((B, C, H + 2 * ph, W + 2 * pw), dtype=x.dtype)
+    xp[:, :, ph:ph + H, pw:pw + W] = x
+    Ho = (H + 2 * ph - kh) // sh + 1
+    Wo = (W + 2 * pw - kw) // sw + 1
+    cols = np.empty((B, C, kh, kw, Ho, Wo), dtype=x.dtype)
+    for ki in range(kh):
+        for kj in range(kw):
+            cols[:, :, ki, kj] = xp[:, :, ki:ki + sh * Ho:sh, kj:kj + sw * Wo:sw]
+    return cols.reshape(B, C * kh * kw, Ho * Wo)
+
+
+def conv_factor_A(x: np.ndarray, kernel, padding, stride, has_bias: bool,
+                  dtype=np.float32) -> np.ndarray:
+    """First factor of a Conv2d layer for one batch.
+
+    models/curvatures.py:341-343,346-349: f = unfold(x).permute(1,0,2).view(Ckk, B*L),
+    ones row if bias, A = f f^T / (B*L).
+    """
+    u = unfold(np.asarray(x, dtype=dtype), kernel, padding, stride)
+    f = np.transpose(u, (1, 0, 2)).reshape(u.shape[1], -1)
+    if has_bias:
+        f = np.concatenate([f, np.ones((1, f.shape[1]), dtype=dtype)], axis=0)
+    return (f @ f.T) / dtype(f.shape[1])
+
+
+class OracleKFAC:
+    """Accumulation semantics of KFAC.update (models/curvatures.py:325-365).
+
+    state[name] = [A, G]; first update assigns, later ones add in place, i.e. the
+    state is a SUM of per-batch means (the batch_size argument is unused).
+    """
+
+    def __init__(self, dtype=np.float32):
+        self.dtype = dtype
+        self.state: dict = {}
+
+    def update_linear(self, name, a, g_rec, has_bias):
+        self._acc(name, linear_factor_A(a, has_bias, self.dtype), grad_factor(g_rec, self.dtype))
+
+    def update_conv(self, name, x, g_rec, kernel, padding, stride, has_bias):
+        self._acc(name, conv_factor_A(x, kernel, padding, stride, has_bias, self.dtype),
+                  grad_factor(g_rec, self.dtype))
+
+    def _acc(self, name, A, G):
+        if name in self.state:
+            self.state[name][0] = self.state[name][0] + A
+            self.state[name][1] = self.state[name][1] + G
+        else:
+            self.state[name] = [A, G]
+
+
+# ------------------------------------------------------------------------ inversion
+def damping_pairs(add, multiply, nlayers):
+    """Argument handling of KFAC.invert (models/curvatures.py:374-378)."""
+    out = []
+    for index in range(nlayers):
+        if not isinstance(add, (float, int)) and not isinstance(multiply, (float, int)):
+            assert len(add) == len(multiply) == nlayers
+            out.append((add[index], multiply[index]))
+        else:
+            out.append((float(add), float(multiply)))
+    return out
+
+
+def damped_factor(F: np.ndarray, n: float, s: float, dtype=np.float64) -> np.ndarray:
+    """R = sqrt(s) F + sqrt(n) I, then (R + R^T)/2 (models/curvatures.py:381-388)."""
+    F = np.asarray(F, dtype=dtype)
+    R = dtype(s ** 0.5) * F + np.diag(np.full(F.shape[0], n ** 0.5, dtype=dtype))
+    return (R + R.T) / dtype(2.0)
+
+
+def inv_chol(R: np.ndarray) -> np.ndarray:
+    """cholesky(inverse(R)) lower (models/curvatures.py:391-392); numpy raises LinAlgError
+    exactly where the reference's numpy fallback (:393-396) would."""
+    return np.linalg.cholesky(np.linalg.inv(R))
+
+
+def invert_factor(F, n, s, dtype=np.float64) -> np.ndarray:
+    return inv_chol(damped_factor(F, n, s, dtype))
+
+
+def spd_inverse_scaled(F, scale, shift, dtype=np.float64) -> np.ndarray:
+    """pinv(scale*(F + tau I)) restated for SPD input as inv(scale F + shift I)
+    (sampling_free/regression/regression_ll_block.py:130-133, shift = scale*tau)."""
+    F = np.asarray(F, dtype=dtype)
+    R = dtype(scale) * F + dtype(shift) * np.eye(F.shape[0], dtype=dtype)
+    R = (R + R.T) / 2
+    return np.linalg.inv(R)
+
+
+# ---------------------------------------------------------------------- eigenvalues
+def get_eigenvalues(factors, dtype=np.float64) -> np.ndarray:
+    """models/utilities.py:120-141: per layer ascending eig of A and G, ger, flatten, cat."""
+    out = []
+    for A, G in factors:
+        la = np.linalg.eigvalsh(np.asarray(A, dtype=dtype))
+        lg = np.linalg.eigvalsh(np.asarray(G, dtype=dtype))
+        out.append(np.outer(la, lg).reshape(-1))
+    return np.concatenate(out) if out else np.zeros(0, dtype=dtype)
+
+
+def get_eigenvectors_sym(F, dtype=np.float64):
+    """models/utilities.py:144-159: eigenvectors of F + F^T (= 2F), ascending."""
+    F = np.asarray(F, dtype=dtype)
+    return np.linalg.eigh(F + F.T)
+
+
+def kron(a, b) -> np.ndarray:
+    """models/utilities.py:387-409 (and torch.kron / sampling_free/utils.py:279-290):
+    kron(a,b)[i*p+k, j*q+l] = a[i,j] * b[k,l]."""
+    a = np.asarray(a)
+    b = np.asarray(b)
+    return np.einsum("ab,cd->acbd", a, b).reshape(a.shape[0] * b.shape[0], a.shape[1] * b.shape[1])
+
+
+# -------------------------------------------------------------- predictive variance
+def kron_quadform(J: np.ndarray, K1: np.ndarray, K2: np.ndarray, dtype=np.float64) -> np.ndarray:
+    """v_b = J_b kron(K1, K2) J_b^T for each row b of J, without forming the kron.
+
+    classification_ll_block.py:128-132: J_i = cat(flatten(dW), db) and
+    H = kron(Q_i, H_i) indexed a*n_G + g, so the product is sum(M * (K1 M K2^T))
+    with M = J_b.reshape(n_A, n_G) (row-major, the reference's flat order).
+    """
+    J = np.atleast_2d(np.asarray(J, dtype=dtype))
+    K1 = np.asarray(K1, dtype=dtype)
+    K2 = np.asarray(K2, dtype=dtype)
+    nA, nG = K1.shape[0], K2.shape[0]
+    M = J.reshape(J.shape[0], nA, nG)
+    return np.einsum("bag,bag->b", M, K1 @ M @ K2.T)
+
+
+def kron_quadform_dense(J, K1, K2, dtype=np.float64):
+    """The reference's literal route (materialised kron) for small cases."""
+    J = np.atleast_2d(np.asarray(J, dtype=dtype))
+    K = kron(np.asarray(K1, dtype=dtype), np.asarray(K2, dtype=dtype))
+    return np.einsum("bi,ij,bj->b", J, K, J)
+
+
+def predictive_std(vs) -> float:
+    """pred_std = sum_l |J_l K_l J_l^T| (classification_ll_block.py:132)."""
+    return float(np.sum(np.abs(vs)))
+
+
+def entropy_bits(pred_std: float) -> float:
+    """0.5*log2(2 pi e var) (classification_ll_block.py:134-135)."""
+    return float(0.5 * np.log2(2 * np.e * np.pi * pred_std))

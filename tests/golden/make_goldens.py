@@ -1,0 +1,326 @@
+"""Generate golden input/output vectors by running the REAL reference read-only.
+
+Run ONLY in the build container (it imports `/root/reference`, which does not
+exist on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py
+
+Every fixture is data (inputs + the reference's outputs) written to
+`tests/golden/*.npz`; no reference source is copied.  The reference code paths
+exercised are:
+
+* `models/curvatures.py:295-323`  KFAC.__init__ + hooks (G5)
+* `models/curvatures.py:325-365`  KFAC.update, Linear + Conv2d (G1, G4, G5)
+* `models/curvatures.py:367-398`  KFAC.invert incl. list damping + numpy fallback (G2)
+* `models/utilities.py:120-141`   get_eigenvalues composition (torch.symeig is gone
+  on torch>=2.0, so eigvalsh is used on the reference's factors, same ascending
+  order, same `ger(...).view(-1)` flattening) (G3)
+* `models/utilities.py:387-409`   kron doctest (G0)
+* `sampling_free/classification/classification_ll_block.py:147-165`
+  predictive-variance loop (no CUDA guard, as in the noise loop) (G6)
+* `sampling_free/regression/regression_ll_block.py:102-140`  regression
+  `pinv(N(q+tau I)) (x) pinv(N(h+tau I))` quadratic form (G7)
+"""
+import os
+import sys
+import warnings
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+sys.dont_write_bytecode = True
+sys.path.insert(0, REF)
+warnings.filterwarnings("ignore")
+
+from models.curvatures import KFAC  # noqa: E402  (reference, read-only)
+from models.utilities import kron as ref_kron  # noqa: E402
+from models.wrapper import BaseNet_750  # noqa: E402
+
+sys.path.insert(0, os.path.join(REF, "sampling_free"))
+
+
+def npf(t):
+    return t.detach().cpu().numpy().copy()
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name)
+    np.savez_compressed(path, **arrays)
+    print(f"wrote {path}: {sum(a.nbytes for a in arrays.values()) / 1e3:.1f} kB raw")
+
+
+def inject_update(kfac, layers, records, batch_size):
+    for layer, (a, g) in zip(layers, records):
+        kfac.record[layer] = [a, g]
+    kfac.update(batch_size=batch_size)
+
+
+# ---------------------------------------------------------------- G0 kron doctest
+def g0_kron():
+    a = torch.tensor([[1, 2], [3, 4]])
+    b = torch.tensor([[0, 5], [6, 7]])
+    rng = np.random.default_rng(7)
+    x = torch.from_numpy(rng.standard_normal((3, 4)).astype(np.float32))
+    y = torch.from_numpy(rng.standard_normal((2, 5)).astype(np.float32))
+    save("g0_kron.npz", a=npf(a), b=npf(b), ab=npf(ref_kron(a, b)),
+         x=npf(x), y=npf(y), xy=npf(ref_kron(x, y)))
+
+
+# ------------------------------------------------- G1a small linear record injection
+def g1_small_linear():
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Linear(20, 12), nn.ReLU(), nn.Linear(12, 5, bias=False))
+    kfac = KFAC(net)
+    layers = [net[0], net[2]]
+    rng = np.random.default_rng(1)
+    out = {}
+    for bi, B in enumerate([16, 16, 7]):
+        a1 = rng.random((B, 20), dtype=np.float32)
+        g1 = rng.standard_normal((B, 12), dtype=np.float32)
+        a2 = rng.random((B, 12), dtype=np.float32)
+        g2 = rng.standard_normal((B, 5), dtype=np.float32)
+        for k, v in dict(a1=a1, g1=g1, a2=a2, g2=g2).items():
+            out[f"b{bi}_{k}"] = v
+        inject_update(kfac, layers, [(torch.from_numpy(a1), torch.from_numpy(g1)),
+                                     (torch.from_numpy(a2), torch.from_numpy(g2))], B)
+    for li, layer in enumerate(layers):
+        out[f"A{li}"], out[f"G{li}"] = npf(kfac.state[layer][0]), npf(kfac.state[layer][1])
+    # invert at the script's damping, the tutorial's and a per-layer list
+    for tag, (add, mult) in {"s": (0.2 ** 2, 200), "t": (1, 200),
+                             "l": ([0.1, 0.3], [10.0, 20.0])}.items():
+        kfac.invert(add, mult)
+        for li, layer in enumerate(layers):
+            LA, LG = kfac.inv_state[layer]
+            out[f"inv{tag}_LA{li}"], out[f"inv{tag}_LG{li}"] = npf(LA), npf(LG)
+    # G3: eigenvalue composition of get_eigenvalues (ascending eigh, ger, flatten, cat)
+    ev = []
+    for layer in layers:
+        A, G = kfac.state[layer]
+        ev.append(torch.ger(torch.linalg.eigvalsh(A), torch.linalg.eigvalsh(G)).contiguous().view(-1))
+    out["eigvals"] = npf(torch.cat(ev))
+    save("g1_small_linear.npz", **out)
+
+
+# ------------------------------------------ G1b MLP 784-128-10 shapes, record injection
+def mlp_batches(seed=123, sizes=(256, 256, 256, 96)):
+    """Seeded synthetic records at MLP shapes (regenerated identically in tests)."""
+    rng = np.random.default_rng(seed)
+    for B in sizes:
+        a1 = rng.random((B, 784), dtype=np.float32)
+        g1 = rng.standard_normal((B, 128), dtype=np.float32)
+        a2 = rng.random((B, 128), dtype=np.float32)
+        g2 = rng.standard_normal((B, 10), dtype=np.float32)
+        yield B, a1, g1, a2, g2
+
+
+def g1_mlp():
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Linear(784, 128), nn.ReLU(), nn.Linear(128, 10))
+    kfac = KFAC(net)
+    layers = [net[0], net[2]]
+    sums = []
+    for B, a1, g1, a2, g2 in mlp_batches():
+        sums.append([float(np.sum(x, dtype=np.float64)) for x in (a1, g1, a2, g2)])
+        inject_update(kfac, layers, [(torch.from_numpy(a1), torch.from_numpy(g1)),
+                                     (torch.from_numpy(a2), torch.from_numpy(g2))], B)
+    A1, G1 = kfac.state[layers[0]]
+    A2, G2 = kfac.state[layers[1]]
+    out = dict(checksums=np.array(sums), A1_diag=npf(torch.diag(A1)), A1_head=npf(A1[:8]),
+               A1_tail=npf(A1[-8:]), A1_eig=np.linalg.eigvalsh(npf(A1).astype(np.float64)),
+               G1=npf(G1), A2=npf(A2), G2=npf(G2))
+    kfac.invert(0.2 ** 2, 200)
+    LA1, LG1 = kfac.inv_state[layers[0]]
+    LA2, LG2 = kfac.inv_state[layers[1]]
+    out.update(LA1_diag=npf(torch.diag(LA1)), LA1_tail=npf(LA1[-8:]), LG1=npf(LG1),
+               LA2=npf(LA2), LG2=npf(LG2))
+    save("g1_mlp.npz", **out)
+
+
+# ------------------------------------------------------------ G2 singular / fallback
+def g2_singular():
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Linear(6, 4))
+    kfac = KFAC(net)
+    rng = np.random.default_rng(5)
+    a = rng.random((2, 6), dtype=np.float32)
+    g = rng.standard_normal((2, 4), dtype=np.float32)
+    inject_update(kfac, [net[0]], [(torch.from_numpy(a), torch.from_numpy(g))], 2)
+    outcome = "ok"
+    try:
+        kfac.invert(0.0, 1.0)
+    except Exception as e:  # record which exception the reference ends in
+        outcome = type(e).__name__
+    res = dict(a=a, g=g, A=npf(kfac.state[net[0]][0]), G=npf(kfac.state[net[0]][1]),
+               outcome=np.array(outcome))
+    if outcome == "ok":
+        LA, LG = kfac.inv_state[net[0]]
+        res.update(LA=npf(LA), LG=npf(LG))
+    save("g2_singular.npz", **res)
+    print("  singular invert(0,1) outcome:", outcome)
+
+
+# ---------------------------------------------------------- G4 conv record injection
+def g4_conv():
+    torch.manual_seed(0)
+
+    class ConvNet(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.c1 = nn.Conv2d(1, 3, 3, stride=1)            # BaseNet_750 conv1
+            self.c2 = nn.Conv2d(3, 6, 3, stride=2)            # BaseNet_750 conv2
+            self.c3 = nn.Conv2d(2, 4, 5, padding=2)           # LeNet-5 conv1 style
+            self.c4 = nn.Conv2d(3, 5, (3, 2), stride=(2, 1), padding=(1, 0), bias=False)
+
+    net = ConvNet()
+    kfac = KFAC(net)
+    rng = np.random.default_rng(11)
+    specs = [(net.c1, (4, 1, 28, 28)), (net.c2, (4, 3, 13, 13)),
+             (net.c3, (3, 2, 9, 9)), (net.c4, (3, 3, 7, 6))]
+    out = {}
+    recs = []
+    for li, (layer, xs) in enumerate(specs):
+        x = rng.random(xs, dtype=np.float32)
+        y = layer(torch.from_numpy(x))
+        g = rng.standard_normal(tuple(y.shape), dtype=np.float32)
+        out[f"x{li}"], out[f"g{li}"] = x, g
+        recs.append((torch.from_numpy(x), torch.from_numpy(g)))
+    inject_update(kfac, [s[0] for s in specs], recs, 0)
+    # second update with the same records pins the "+=" accumulation
+    inject_update(kfac, [s[0] for s in specs], recs, 0)
+    for li, (layer, _) in enumerate(specs):
+        out[f"A{li}"], out[f"G{li}"] = npf(kfac.state[layer][0]), npf(kfac.state[layer][1])
+        out[f"meta{li}"] = np.array([layer.kernel_size[0], layer.kernel_size[1], layer.stride[0],
+                                     layer.stride[1], layer.padding[0], layer.padding[1],
+                                     int(layer.bias is not None), layer.out_channels])
+    save("g4_conv.npz", **out)
+
+
+# ------------------------------------------------- G5 e2e hooks on BaseNet_750 (+G6)
+def gradient(y, x, grad_outputs):
+    # same call as sampling_free/utils.py:221-226
+    return torch.autograd.grad(y, [x], grad_outputs=grad_outputs, create_graph=True,
+                               retain_graph=True, allow_unused=True)[0]
+
+
+def g5_g6_basenet():
+    torch.manual_seed(3)
+    net = BaseNet_750()
+    net.weight_init_uniform(0.2)
+    weights = {k: npf(v) for k, v in net.state_dict().items()}
+    kfac = KFAC(net)
+    criterion = nn.CrossEntropyLoss()
+    rng = np.random.default_rng(21)
+    out = {f"w_{k}": v for k, v in weights.items()}
+    for bi in range(2):
+        x = rng.random((8, 1, 28, 28), dtype=np.float32)
+        logits = net(torch.from_numpy(x))
+        labels = torch.distributions.Categorical(logits=logits).sample()  # script :95-97
+        loss = criterion(logits, labels)
+        net.zero_grad()
+        loss.backward()
+        kfac.update(batch_size=8)
+        out[f"x{bi}"], out[f"y{bi}"] = x, npf(labels)
+    layers = [net.conv1, net.conv2, net.fc1]
+    for li, layer in enumerate(layers):
+        out[f"A{li}"], out[f"G{li}"] = npf(kfac.state[layer][0]), npf(kfac.state[layer][1])
+    kfac.invert(0.2 ** 2, 200)
+    for li, layer in enumerate(layers):
+        LA, LG = kfac.inv_state[layer]
+        out[f"LA{li}"], out[f"LG{li}"] = npf(LA), npf(LG)
+    # G6: classification predictive variance, batch 1 and batch 8 (script :147-165)
+    for tag, nb in (("b1", 1), ("b8", 8)):
+        x = torch.from_numpy(rng.random((nb, 1, 28, 28), dtype=np.float32))
+        pred_mean = torch.softmax(net(x), dim=1)
+        idx = np.argmax(npf(pred_mean), axis=1)
+        grad_outputs = torch.zeros_like(pred_mean)
+        grad_outputs[:, idx] = 1
+        pred_std = 0
+        vs = []
+        for li, layer in enumerate(layers):
+            Q_i, H_i = kfac.inv_state[layer]
+            g = [torch.flatten(gradient(pred_mean, p, grad_outputs)) for p in layer.parameters()]
+            J_i = torch.cat(g, dim=0).unsqueeze(0)
+            H = torch.kron(Q_i, H_i)
+            v = (J_i @ H @ J_i.t()).item()
+            vs.append(v)
+            pred_std += abs(v)
+            out[f"var_{tag}_J{li}"] = npf(J_i[0])
+        out[f"var_{tag}_x"] = npf(x)
+        out[f"var_{tag}_v"] = np.array(vs)
+        out[f"var_{tag}_std"] = np.array(pred_std)
+        out[f"var_{tag}_entropy"] = np.array(0.5 * np.log2(2 * np.e * np.pi * pred_std))
+    save("g5_basenet750.npz", **out)
+
+
+# --------------------------------------------------------------- G7 regression block
+def g7_regression():
+    # Net 1-30-30-1 as in regression_ll_block.py:23-34 (same shapes, own definition)
+    class Net(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.fc1, self.fc2, self.fc3 = nn.Linear(1, 30), nn.Linear(30, 30), nn.Linear(30, 1)
+
+        def forward(self, x):
+            return self.fc3(F.relu(self.fc2(F.relu(self.fc1(x)))))
+
+    torch.manual_seed(2)
+    x = torch.FloatTensor(30, 1).uniform_(-4, 4).sort(dim=0).values
+    y = x.pow(3) + 3 * torch.rand(x.size())
+    net = Net()
+    for m in net.modules():
+        if isinstance(m, nn.Linear):
+            nn.init.uniform_(m.weight, -0.2, 0.2)
+            m.bias.data.fill_(0)
+    opt = torch.optim.SGD(net.parameters(), lr=1e-3)
+    kfac = KFAC(net)
+    for _ in range(25):  # shortened training loop (script runs 10000)
+        loss = F.mse_loss(net(x), y)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        kfac.update(batch_size=1)
+    N, tau, sigma = 30, 0.01, 3
+    from utils import kronecker_product  # sampling_free/utils.py:279-290
+    xs = torch.linspace(-6, 6, 9).unsqueeze(1)
+    layers = [net.fc1, net.fc2, net.fc3]
+    out = {f"w_{k}": npf(v) for k, v in net.state_dict().items()}
+    for li, layer in enumerate(layers):
+        out[f"q{li}"], out[f"h{li}"] = npf(kfac.state[layer][0]), npf(kfac.state[layer][1])
+    stds, vs = [], []
+    for j, x_j in enumerate(xs):
+        pred_j = net(x_j)
+        std_j = 0
+        row = []
+        for li, layer in enumerate(layers):
+            q_i, h_i = kfac.state[layer]
+            q_inv = torch.pinverse(N * (q_i + torch.diag(tau * torch.ones(q_i.shape[0]))))
+            h_inv = torch.pinverse(N * (h_i + torch.diag(tau * torch.ones(h_i.shape[0]))))
+            g = []
+            for p in layer.parameters():  # regression_ll_block.py:65-76 jacobian, 1 output
+                go = torch.zeros_like(pred_j)
+                go[0] = 1
+                g.append(torch.flatten(gradient(pred_j, p, go)))
+            J_i = torch.cat(g, dim=0).unsqueeze(0)
+            v = (J_i @ kronecker_product(q_inv, h_inv) @ J_i.t()).item()
+            row.append(v)
+            std_j += abs(v)
+            out[f"J_{j}_{li}"] = npf(J_i[0])
+        vs.append(row)
+        stds.append(std_j ** 0.5 + sigma)
+    out.update(xs=npf(xs), v=np.array(vs), std=np.array(stds), N=np.array(N),
+               tau=np.array(tau), sigma=np.array(sigma))
+    save("g7_regression.npz", **out)
+
+
+if __name__ == "__main__":
+    g0_kron()
+    g1_small_linear()
+    g1_mlp()
+    g2_singular()
+    g4_conv()
+    g5_g6_basenet()
+    g7_regression()
