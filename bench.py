@@ -1,0 +1,248 @@
+#!/usr/bin/env python
+"""Benchmark: images/sec for one full KFAC factor pass + factor inversion (MNIST MLP).
+
+    python bench.py [--gpus N --steps K --warmup W] [--config mlp|lenet|wide]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+One STEP = one KFAC data pass over `--images` synthetic images per rank in batches
+of `--batch` (one KFAC.update per batch, activations/gradients already resident in
+HBM, records injected exactly as the reference's hooks leave them) + the packed
+RCCL all-reduce (N > 1) + KFAC.invert(0.04, 200) (models/curvatures.py:325-398;
+damping of classification_ll_block.py:72-73,106).  Weak scaling: every rank
+processes the same per-rank workload; `value` = all ranks' images / wall time.
+
+Also reported (same JSON line): the roofline of the dominant kernel
+(kfac_factor_tiles, fp32 MFMA; HIP-event durations measured live on its stream),
+the pass/invert split, an end-to-end variant (forward + Categorical label sample
++ CE backward + update + invert), and the CPU baseline: the reference's op
+sequence (oracle/cpu_ref_torch.py, torch CPU fp32) on a bounded sample of the
+same workload, on this host's cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "images/sec for full KFAC factor pass + factor inversion, MNIST MLP, 1/2/4/8 GPUs"
+MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md, chip table)
+DAMPING = (0.2 ** 2, 200)     # invert(std**2, N), classification_ll_block.py:72-73,106
+
+
+def layer_dims(config):
+    """(d_in, d_out) of the KFAC'd Linear layers."""
+    if config == "mlp":
+        return [(784, 128), (128, 10)]
+    if config == "wide":
+        return [(784, 4096), (4096, 4096), (4096, 10)]
+    raise ValueError(config)
+
+
+def flops_per_image(dims):
+    """Algorithmic SYRK work: sum_layers n_A(n_A+1) + n_G(n_G+1) (lower triangle incl.
+    the bias ones column)."""
+    return sum((a + 1) * (a + 2) + g * (g + 1) for a, g in dims)
+
+
+def bytes_per_image(dims):
+    return sum(4 * (a + g) for a, g in dims)
+
+
+def build_model(config, device):
+    """Random-init MLP of the configured shape (default torch init, seed 0)."""
+    torch.manual_seed(0)
+    mods, dims = [], layer_dims(config)
+    for i, (d_in, d_out) in enumerate(dims):
+        mods.append(torch.nn.Linear(d_in, d_out))
+        if i + 1 < len(dims):
+            mods.append(torch.nn.ReLU())
+    return torch.nn.Sequential(*mods).to(device)
+
+
+def synthetic_records(dims, images, device, seed):
+    """Resident activations U[0,1) (post-ReLU-like) and gradient records N(0,1)."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    recs = []
+    for d_in, d_out in dims:
+        a = torch.rand(images, d_in, device=device, generator=g)
+        gr = torch.randn(images, d_out, device=device, generator=g)
+        recs.append((a, gr))
+    return recs
+
+
+def cpu_baseline(dims, images, batch, budget_s=12.0):
+    """The reference's CPU op sequence (oracle/cpu_ref_torch.py) on the same workload,
+    bounded to ~budget_s seconds; returns (images/s, cores, sample description)."""
+    from oracle import cpu_ref_torch as C
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    rng = np.random.default_rng(0)
+    recs = [(torch.from_numpy(rng.random((images, a), dtype=np.float32)),
+             torch.from_numpy(rng.standard_normal((images, g), dtype=np.float32))) for a, g in dims]
+    done, t0 = 0, time.perf_counter()
+    passes = 0
+    while True:
+        state = {}
+        for i in range(0, images, batch):
+            for li, (a, gr) in enumerate(recs):
+                C.linear_update(state, li, a[i:i + batch], gr[i:i + batch], True)
+        C.invert(state, *DAMPING)
+        done += images
+        passes += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return done / dt, threads, (f"{passes} full pass(es) of {images} synthetic images, batch {batch}, "
+                                f"update+invert, torch {torch.__version__} CPU fp32, {threads} threads")
+
+
+def load_traffic():
+    path = os.path.join(ROOT, "profiles", "factor_tiles_pmc.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="mlp", choices=["mlp", "wide"])
+    ap.add_argument("--batch", type=int, default=4096, help="per-rank batch")
+    ap.add_argument("--images", type=int, default=60000, help="images per rank per pass")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    from bnn_kfac_amd import _native as N
+    from bnn_kfac_amd.curvatures import KFAC
+    from bnn_kfac_amd.distributed import DistributedKFAC
+
+    dims = layer_dims(args.config)
+    net = build_model(args.config, device)
+    layers = [m for m in net.modules() if isinstance(m, torch.nn.Linear)]
+    kfac = DistributedKFAC(net) if world > 1 else KFAC(net)
+    recs = synthetic_records(dims, args.images, device, seed=1234 + rank)
+    starts = list(range(0, args.images, args.batch))
+
+    def one_pass():
+        kfac.reset()
+        for i in starts:
+            for layer, (a, g) in zip(layers, recs):
+                kfac.record[layer] = [a[i:i + args.batch], g[i:i + args.batch]]
+            kfac.update(batch_size=min(args.batch, args.images - i))
+        kfac.invert(*DAMPING)
+
+    def sync():
+        torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        one_pass()
+    sync()
+    N.profile_reset()
+    N.profile_enable(True)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_pass()
+    sync()
+    elapsed = time.perf_counter() - t0
+    N.profile_enable(False)
+    tiles_ms, tiles_n = N.profile_read(N.PROF_FACTOR_TILES)
+    red_ms, red_n = N.profile_read(N.PROF_FACTOR_REDUCE)
+    inv_ms, inv_n = N.profile_read(N.PROF_INVERT)
+    N.profile_reset()
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+
+    images_total = world * args.images * args.steps
+    value = images_total / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+
+    # roofline of the dominant kernel: algorithmic flops of one launch (= one
+    # update of one batch) / its measured duration, averaged over the timed region
+    fpi = flops_per_image(dims)
+    flops_timed = fpi * args.images * args.steps
+    achieved = flops_timed / (tiles_ms * 1e-3) / 1e12 if tiles_ms > 0 else None
+    traffic = load_traffic()
+    roofline = {"bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": (achieved / MFMA_F32_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
+                "kernel": "kfac_factor_tiles", "launches": tiles_n,
+                "avg_launch_us": 1e3 * tiles_ms / max(tiles_n, 1),
+                "flops_per_launch": fpi * args.batch,
+                "algorithmic_bytes_per_launch": bytes_per_image(dims) * args.batch}
+    breakdown = {"factor_tiles_ms_per_step": tiles_ms / args.steps,
+                 "factor_reduce_ms_per_step": red_ms / args.steps,
+                 "invert_ms_per_step": inv_ms / args.steps,
+                 "updates_per_step": len(starts)}
+
+    e2e = None
+    if not args.no_e2e and world == 1:
+        x = torch.rand(args.images, 784, device=device)
+        crit = torch.nn.CrossEntropyLoss()
+
+        def e2e_pass():
+            kfac.reset()
+            for i in starts:
+                logits = net(x[i:i + args.batch])
+                labels = torch.distributions.Categorical(logits=logits).sample()
+                loss = crit(logits, labels)
+                net.zero_grad()
+                loss.backward()
+                kfac.update(batch_size=logits.shape[0])
+            kfac.invert(*DAMPING)
+        e2e_pass()
+        sync()
+        t1 = time.perf_counter()
+        reps = max(1, args.steps // 2)
+        for _ in range(reps):
+            e2e_pass()
+        sync()
+        e2e = args.images * reps / (time.perf_counter() - t1)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        v, cores, sample = cpu_baseline(dims, args.images, args.batch)
+        cpu = {"value": v, "unit": "images/s", "cores": cores, "kind": "port", "sample": sample}
+
+    if rank == 0:
+        out = {"metric": METRIC, "value": value, "unit": "images/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+               "data": "synthetic (resident U[0,1) activations, N(0,1) output-gradient records)",
+               "config": {"workload": f"{args.config.upper()} {'-'.join(str(d[0]) for d in dims)}-10 KFAC factor "
+                                      f"pass over {args.images} images/rank (batch {args.batch}/rank) + "
+                                      f"invert{DAMPING}",
+                          "global_batch": args.batch * world, "images_per_rank": args.images,
+                          "parallelism": f"dp{world}"},
+               "roofline": roofline, "cpu_baseline": cpu, "breakdown": breakdown,
+               "e2e_images_per_s": e2e}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

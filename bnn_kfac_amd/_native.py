@@ -1,0 +1,284 @@
+"""ctypes binding of libkfac_hip.so (the C ABI declared in include/kfac_hip.h).
+
+The product path has NO fallback: if the library is missing, fails to load, or a
+tensor is not on a HIP device, the calls below raise.  Device buffers are torch
+tensors (the caching allocator owns them); the stream is torch's current stream
+on the tensor's device, passed to every call explicitly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("BNN_KFAC_AMD_LIB", os.path.join(_HERE, "libkfac_hip.so"))
+
+# enums (include/kfac_hip.h)
+KFAC_OK, KFAC_EINVAL, KFAC_ELAUNCH, KFAC_EWORKSPACE = 0, -1, -2, -3
+ROWMAJOR, CHANNEL, PATCH = 0, 1, 2
+OUT_INV_CHOL, OUT_INVERSE = 0, 1
+PROF_FACTOR_TILES, PROF_FACTOR_REDUCE, PROF_INVERT, PROF_QUAD_TILES = 0, 1, 2, 3
+
+c_i32, c_i64, c_f32, c_f64, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_void_p
+
+
+class Operand(ctypes.Structure):
+    _fields_ = [("ptr", c_vp), ("layout", c_i32), ("cols", c_i32), ("rows", c_i64),
+                ("has_ones", c_i32), ("reserved0", c_i32), ("ld", c_i64), ("L", c_i64),
+                ("sB", c_i64)] + [(f, c_i32) for f in
+                                  ("C", "H", "W", "kh", "kw", "sh", "sw", "ph", "pw", "Ho", "Wo",
+                                   "reserved1")]
+
+
+class FactorJob(ctypes.Structure):
+    _fields_ = [("x", Operand), ("alpha", c_f32), ("beta", c_f32), ("F", c_vp), ("ldF", c_i64)]
+
+
+class InvertJob(ctypes.Structure):
+    _fields_ = [("F", c_vp), ("ldF", c_i64), ("n", c_i32), ("out_kind", c_i32),
+                ("scale", c_f64), ("shift", c_f64), ("out", c_vp), ("ldo", c_i64)]
+
+
+class EigJob(ctypes.Structure):
+    _fields_ = [("F", c_vp), ("ldF", c_i64), ("n", c_i32), ("reserved", c_i32),
+                ("evals", c_vp), ("evecs", c_vp), ("ldv", c_i64)]
+
+
+class QuadJob(ctypes.Structure):
+    _fields_ = [("J", c_vp), ("ldJ", c_i64), ("nA", c_i32), ("nG", c_i32), ("K1", c_vp),
+                ("ld1", c_i64), ("K2", c_vp), ("ld2", c_i64), ("lower1", c_i32),
+                ("lower2", c_i32), ("v", c_vp)]
+
+
+# symbol -> (restype, argtypes); every symbol include/kfac_hip.h declares
+SIGNATURES = {
+    "kfac_factor_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(FactorJob), ctypes.c_int]),
+    "kfac_factor_update": (ctypes.c_int, [ctypes.POINTER(FactorJob), ctypes.c_int, c_vp,
+                                          ctypes.c_size_t, c_vp]),
+    "kfac_syrk_linear": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, ctypes.c_int, c_f32, c_f32,
+                                        c_vp, c_i64, c_vp, ctypes.c_size_t, c_vp]),
+    "kfac_syrk_conv": (ctypes.c_int, [c_vp, c_i64] + [ctypes.c_int] * 10 + [c_f32, c_f32, c_vp,
+                                                                            c_i64, c_vp,
+                                                                            ctypes.c_size_t, c_vp]),
+    "kfac_syrk_convgrad": (ctypes.c_int, [c_vp, c_i64, ctypes.c_int, c_i64, c_f32, c_f32, c_vp,
+                                          c_i64, c_vp, ctypes.c_size_t, c_vp]),
+    "kfac_invert_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(InvertJob), ctypes.c_int]),
+    "kfac_invert": (ctypes.c_int, [ctypes.POINTER(InvertJob), ctypes.c_int, c_vp,
+                                   ctypes.c_size_t, c_vp, c_vp]),
+    "kfac_damped_inv_chol": (ctypes.c_int, [c_vp, ctypes.c_int, c_i64, c_f64, c_f64, c_vp, c_i64,
+                                            c_vp, ctypes.c_size_t, c_vp, c_vp]),
+    "kfac_eig_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(EigJob), ctypes.c_int]),
+    "kfac_syev": (ctypes.c_int, [ctypes.POINTER(EigJob), ctypes.c_int, c_vp, ctypes.c_size_t,
+                                 c_vp, c_vp]),
+    "kfac_quadform_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(QuadJob), ctypes.c_int,
+                                                        c_i64]),
+    "kfac_kron_quadform": (ctypes.c_int, [ctypes.POINTER(QuadJob), ctypes.c_int, c_i64,
+                                          ctypes.c_int, c_vp, c_vp, ctypes.c_size_t, c_vp]),
+    "kfac_profile_enable": (ctypes.c_int, [ctypes.c_int]),
+    "kfac_profile_read": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(ctypes.c_int64)]),
+    "kfac_profile_reset": (ctypes.c_int, []),
+    "kfac_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "kfac_version": (ctypes.c_char_p, []),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libkfac_hip.so (after torch, so the process shares torch's HIP runtime)."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise NativeError(
+                        f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; "
+                        f"g.build()'` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+                handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+                for name, (res, args) in SIGNATURES.items():
+                    fn = getattr(handle, name)
+                    fn.restype = res
+                    fn.argtypes = args
+                _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != KFAC_OK:
+        msg = lib().kfac_strerror(rc).decode()
+        raise NativeError(f"{what} failed: {msg} ({rc})")
+
+
+def require_device(t: torch.Tensor, what: str):
+    if not t.is_cuda:
+        raise NativeError(f"bnn_kfac_amd runs on the MI355X only: {what} is on {t.device} "
+                          f"(no CPU fallback; move the model/tensors to a HIP device)")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{what}: expected float32 (the reference computes in fp32), got {t.dtype}")
+
+
+def stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class _Workspace:
+    """Grow-only device scratch per (device, stream); stream order makes reuse safe."""
+
+    def __init__(self):
+        self._bufs = {}
+
+    def get(self, device: torch.device, nbytes: int) -> torch.Tensor:
+        key = (device.index, stream_handle(device))
+        buf = self._bufs.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+            self._bufs[key] = buf
+        return buf
+
+
+workspace = _Workspace()
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def as_array(ctype, items):
+    arr = (ctype * len(items))()
+    for i, it in enumerate(items):
+        arr[i] = it
+    return arr
+
+
+# ------------------------------------------------------------------ op wrappers
+def factor_update(jobs, device: torch.device):
+    if not jobs:
+        return
+    L = lib()
+    arr = as_array(FactorJob, jobs)
+    need = L.kfac_factor_workspace_bytes(arr, len(jobs))
+    ws = workspace.get(device, need)
+    check(L.kfac_factor_update(arr, len(jobs), ptr(ws), ws.numel(), stream_handle(device)),
+          "kfac_factor_update")
+
+
+def invert(jobs, device: torch.device) -> torch.Tensor:
+    """Launch the grouped inversion; returns the DEVICE info tensor (int32, one per job)."""
+    L = lib()
+    arr = as_array(InvertJob, jobs)
+    need = L.kfac_invert_workspace_bytes(arr, len(jobs))
+    ws = workspace.get(device, need)
+    info = torch.zeros(len(jobs), dtype=torch.int32, device=device)
+    check(L.kfac_invert(arr, len(jobs), ptr(ws), ws.numel(), ptr(info), stream_handle(device)),
+          "kfac_invert")
+    return info
+
+
+def syev(jobs, device: torch.device) -> torch.Tensor:
+    L = lib()
+    arr = as_array(EigJob, jobs)
+    need = L.kfac_eig_workspace_bytes(arr, len(jobs))
+    ws = workspace.get(device, need)
+    info = torch.zeros(len(jobs), dtype=torch.int32, device=device)
+    check(L.kfac_syev(arr, len(jobs), ptr(ws), ws.numel(), ptr(info), stream_handle(device)),
+          "kfac_syev")
+    return info
+
+
+def kron_quadform(jobs, nb: int, abs_sum: bool, out: torch.Tensor):
+    L = lib()
+    arr = as_array(QuadJob, jobs)
+    need = L.kfac_quadform_workspace_bytes(arr, len(jobs), nb)
+    ws = workspace.get(out.device, need)
+    check(L.kfac_kron_quadform(arr, len(jobs), nb, int(abs_sum), ptr(out), ptr(ws), ws.numel(),
+                               stream_handle(out.device)), "kfac_kron_quadform")
+
+
+# ---------------------------------------------------------------- job builders
+def rowmajor_operand(x: torch.Tensor, has_ones: bool) -> Operand:
+    """(rows, cols) row-major matrix, unit column stride (Linear a / g_rec)."""
+    assert x.dim() == 2 and x.stride(1) == 1
+    op = Operand()
+    op.ptr, op.layout, op.rows, op.cols = x.data_ptr(), ROWMAJOR, x.shape[0], x.shape[1]
+    op.ld = max(x.stride(0), x.shape[1])
+    op.has_ones = int(has_ones)
+    return op
+
+
+def channel_operand(g: torch.Tensor) -> Operand:
+    """Conv2d output gradient (B, C, Ho, Wo) contiguous: rows = B*Ho*Wo, cols = C."""
+    assert g.dim() == 4 and g.is_contiguous()
+    B, C, Ho, Wo = g.shape
+    op = Operand()
+    op.ptr, op.layout, op.cols = g.data_ptr(), CHANNEL, C
+    op.L = Ho * Wo
+    op.sB = C * Ho * Wo
+    op.rows = B * Ho * Wo
+    return op
+
+
+def patch_operand(x: torch.Tensor, kernel, padding, stride, has_ones: bool) -> Operand:
+    """Implicit F.unfold(x, kernel, padding=, stride=) of a contiguous (B,C,H,W) input."""
+    assert x.dim() == 4 and x.is_contiguous()
+    B, C, H, W = x.shape
+    kh, kw = kernel
+    ph, pw = padding
+    sh, sw = stride
+    Ho = (H + 2 * ph - kh) // sh + 1
+    Wo = (W + 2 * pw - kw) // sw + 1
+    if Ho <= 0 or Wo <= 0:
+        raise RuntimeError(f"unfold: kernel {kernel} with padding {padding} larger than input {H}x{W}")
+    op = Operand()
+    op.ptr, op.layout = x.data_ptr(), PATCH
+    op.C, op.H, op.W, op.kh, op.kw, op.sh, op.sw, op.ph, op.pw, op.Ho, op.Wo = \
+        C, H, W, kh, kw, sh, sw, ph, pw, Ho, Wo
+    op.L = Ho * Wo
+    op.sB = C * H * W
+    op.rows = B * Ho * Wo
+    op.cols = C * kh * kw
+    op.has_ones = int(has_ones)
+    return op
+
+
+def factor_job(op: Operand, F: torch.Tensor, alpha: float, beta: float) -> FactorJob:
+    j = FactorJob()
+    j.x = op
+    j.alpha, j.beta = alpha, beta
+    j.F = F.data_ptr()
+    j.ldF = F.stride(0)
+    return j
+
+
+def invert_job(F: torch.Tensor, out: torch.Tensor, scale: float, shift: float,
+               kind: int = OUT_INV_CHOL) -> InvertJob:
+    j = InvertJob()
+    j.F, j.ldF, j.n, j.out_kind = F.data_ptr(), F.stride(0), F.shape[0], kind
+    j.scale, j.shift = scale, shift
+    j.out, j.ldo = out.data_ptr(), out.stride(0)
+    return j
+
+
+# ------------------------------------------------------------------ profiling
+def profile_enable(on: bool = True):
+    check(lib().kfac_profile_enable(int(on)), "kfac_profile_enable")
+
+
+def profile_reset():
+    check(lib().kfac_profile_reset(), "kfac_profile_reset")
+
+
+def profile_read(kid: int):
+    """(total milliseconds, launches) of the library's launches of kernel `kid`
+    recorded since the last reset (HIP events on the launch stream)."""
+    ms, n = ctypes.c_double(), ctypes.c_int64()
+    check(lib().kfac_profile_read(kid, ctypes.byref(ms), ctypes.byref(n)), "kfac_profile_read")
+    return ms.value, n.value

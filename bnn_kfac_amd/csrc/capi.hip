@@ -1,0 +1,101 @@
+// Misc C-ABI entry points of libkfac_hip.so.
+#include "kfac_common.h"
+
+extern "C" const char* kfac_strerror(int status) {
+  switch (status) {
+    case KFAC_OK: return "ok";
+    case KFAC_EINVAL: return "invalid argument";
+    case KFAC_ELAUNCH: return "HIP kernel launch failed";
+    case KFAC_EWORKSPACE: return "workspace too small";
+    default: return "unknown kfac status";
+  }
+}
+
+extern "C" const char* kfac_version(void) { return "bnn_kfac_amd 0.1.0 gfx950"; }
+
+// ------------------------------------------------------------------ profiling
+#include <mutex>
+#include <vector>
+
+namespace kfac {
+namespace {
+struct Rec {
+  int id;
+  hipEvent_t start, stop;
+};
+std::mutex g_mu;
+bool g_on = false;
+std::vector<Rec> g_open;     // started, waiting for their stop
+std::vector<Rec> g_done;     // closed pairs, read lazily
+std::vector<hipEvent_t> g_pool;
+
+hipEvent_t take() {
+  if (!g_pool.empty()) {
+    hipEvent_t e = g_pool.back();
+    g_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+}  // namespace
+
+void prof_begin(int id, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_on) return;
+  Rec r{id, take(), take()};
+  if (!r.start || !r.stop) return;
+  (void)hipEventRecord(r.start, s);
+  g_open.push_back(r);
+}
+
+void prof_end(int id, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_on) return;
+  for (size_t i = g_open.size(); i-- > 0;) {
+    if (g_open[i].id == id) {
+      (void)hipEventRecord(g_open[i].stop, s);
+      g_done.push_back(g_open[i]);
+      g_open.erase(g_open.begin() + i);
+      return;
+    }
+  }
+}
+}  // namespace kfac
+
+using namespace kfac;
+
+extern "C" int kfac_profile_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_on = on != 0;
+  return KFAC_OK;
+}
+
+extern "C" int kfac_profile_read(int id, double* total_ms, int64_t* launches) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  double tot = 0.0;
+  int64_t cnt = 0;
+  for (const Rec& r : g_done) {
+    if (r.id != id) continue;
+    if (hipEventSynchronize(r.stop) != hipSuccess) return KFAC_ELAUNCH;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, r.start, r.stop) != hipSuccess) return KFAC_ELAUNCH;
+    tot += ms;
+    ++cnt;
+  }
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = cnt;
+  return KFAC_OK;
+}
+
+extern "C" int kfac_profile_reset(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (const Rec& r : g_done) {
+    (void)hipEventSynchronize(r.stop);
+    g_pool.push_back(r.start);
+    g_pool.push_back(r.stop);
+  }
+  g_done.clear();
+  return KFAC_OK;
+}

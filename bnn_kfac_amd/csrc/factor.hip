@@ -1,0 +1,300 @@
+// Kronecker-factor accumulation (KFAC.update) on gfx950.
+//
+// Replaces models/curvatures.py:341-363: per layer A = [a 1]^T[a 1]/cols and
+// G = g^T g/cols (Conv2d through an implicit im2col / channel-major view instead
+// of F.unfold + permute().contiguous() copies), then state = state + factor.
+//
+// One KFAC.update() = two launches for ALL layers' factors:
+//   1. kfac_factor_tiles : grouped split-K fp32-MFMA SYRK.  A task is one
+//      64x64 lower-triangle tile of one factor over one K-chunk; it writes a
+//      64x64 fp32 partial slab (deterministic, no atomics).
+//   2. kfac_factor_reduce: per tile, sum the slabs in split order, apply
+//      F = beta*F + alpha*sum, write the tile and its mirror (LDS transpose),
+//      so F stays exactly symmetric.
+#include "kfac_common.h"
+
+namespace kfac {
+
+constexpr int MAXJ = 8;  // factor jobs per launch (kernarg budget)
+
+struct FactorJobDev {
+  OpDev x;
+  float alpha, beta;
+  float* F;
+  int64_t ldF;
+  float* slab;       // this job's slabs: tiles*splits x 64 x 64
+  int64_t chunk;     // rows per split (multiple of BK)
+  int n, t, splits;  // factor edge, tiles per edge, K-splits
+  int task_begin;    // first global task of this job
+  int tile_begin;    // first global tile of this job (reduce launch)
+};
+
+struct FactorArgs {
+  int njobs;
+  int task_end[MAXJ];
+  int tile_end[MAXJ];
+  FactorJobDev job[MAXJ];
+};
+
+template <int LAYOUT>
+__device__ __forceinline__ void factor_task(const FactorJobDev& J, int local, float* lds) {
+  const int tile = local / J.splits, split = local - tile * J.splits;
+  int ti, tj;
+  tri_decode(tile, ti, tj);
+  const int64_t k0 = (int64_t)split * J.chunk;
+  const int64_t k1 = min(J.x.rows, k0 + J.chunk);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int qi = wave >> 1, qj = wave & 1;
+  const bool diag = ti == tj;
+  const bool active = !(diag && qi < qj);  // strictly-upper quadrant of a diagonal tile
+  floatx16 acc;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+  contract_tile<LAYOUT, LAYOUT>(J.x, ti * TILE, J.x, tj * TILE, k0, k1, diag, active, lds, acc);
+  if (!active) return;
+  float* out = J.slab + (size_t)local * TILE * TILE;
+  const int col = qj * 32 + (lane & 31);
+#pragma unroll
+  for (int v = 0; v < 16; ++v) out[(qi * 32 + acc_row(v, lane)) * TILE + col] = acc[v];
+}
+
+__global__ __launch_bounds__(NTHREADS) void kfac_factor_tiles(FactorArgs args) {
+  __shared__ __attribute__((aligned(16))) float lds[4 * PANEL];
+  const int task = blockIdx.x;
+  int j = 0;
+  while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
+  const FactorJobDev& J = args.job[j];
+  const int local = task - J.task_begin;
+  switch (J.x.layout) {
+    case KFAC_ROWMAJOR: factor_task<KFAC_ROWMAJOR>(J, local, lds); break;
+    case KFAC_CHANNEL: factor_task<KFAC_CHANNEL>(J, local, lds); break;
+    default: factor_task<KFAC_PATCH>(J, local, lds); break;
+  }
+}
+
+__global__ __launch_bounds__(NTHREADS) void kfac_factor_reduce(FactorArgs args) {
+  __shared__ float tileT[TILE * LDP];
+  const int gtile = blockIdx.x;
+  int j = 0;
+  while (j + 1 < args.njobs && gtile >= args.tile_end[j]) ++j;
+  const FactorJobDev& J = args.job[j];
+  const int tile = gtile - J.tile_begin;
+  int ti, tj;
+  tri_decode(tile, ti, tj);
+  const int i0 = ti * TILE, j0 = tj * TILE;
+  const bool diag = ti == tj;
+  const float* slab = J.slab + (size_t)tile * J.splits * TILE * TILE;
+  const float alpha = J.alpha, beta = J.beta;
+  for (int e = threadIdx.x; e < TILE * TILE; e += NTHREADS) {
+    const int r = e >> 6, c = e & 63;
+    const int gi = i0 + r, gj = j0 + c;
+    if (gi >= J.n || gj >= J.n || (diag && c > r)) continue;
+    float s = 0.f;
+    for (int sp = 0; sp < J.splits; ++sp) s += slab[(size_t)sp * TILE * TILE + e];
+    float* f = J.F + (int64_t)gi * J.ldF + gj;
+    const float val = beta == 0.f ? alpha * s : beta * (*f) + alpha * s;
+    *f = val;
+    tileT[r * LDP + c] = val;
+  }
+  if (diag) {  // mirror inside the diagonal tile
+    __syncthreads();
+    for (int e = threadIdx.x; e < TILE * TILE; e += NTHREADS) {
+      const int r = e >> 6, c = e & 63;  // write (r, c) for c > r from (c, r)
+      const int gi = i0 + r, gj = j0 + c;
+      if (c > r && gi < J.n && gj < J.n) J.F[(int64_t)gi * J.ldF + gj] = tileT[c * LDP + r];
+    }
+    return;
+  }
+  __syncthreads();
+  // mirrored tile (j0.., i0..), coalesced along its rows
+  for (int e = threadIdx.x; e < TILE * TILE; e += NTHREADS) {
+    const int r = e >> 6, c = e & 63;
+    const int gi = j0 + r, gj = i0 + c;
+    if (gi < J.n && gj < J.n) J.F[(int64_t)gi * J.ldF + gj] = tileT[c * LDP + r];
+  }
+}
+
+// ------------------------------------------------------------------- host side
+struct Plan {
+  int tiles, splits;
+  int64_t chunk;
+  size_t slab_bytes;
+};
+
+static int factor_n(const kfac_factor_job& j) { return j.x.cols + (j.x.has_ones ? 1 : 0); }
+
+// Split K so that the whole grouped launch has ~4 tasks per CU (256 CUs) but
+// every task still runs >= 256 rows of MFMA work.
+static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans) {
+  int64_t work = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const int t = (int)cdiv(factor_n(jobs[i]), TILE);
+    work += (int64_t)t * (t + 1) / 2 * cdiv(jobs[i].x.rows, BK);
+  }
+  const int64_t target_tasks = 1024;
+  int64_t chunk_steps = std::max<int64_t>(8, cdiv(work, target_tasks));  // in BK units
+  for (int i = 0; i < njobs; ++i) {
+    const int t = (int)cdiv(factor_n(jobs[i]), TILE);
+    Plan& p = plans[i];
+    p.tiles = t * (t + 1) / 2;
+    const int64_t steps = std::max<int64_t>(1, cdiv(jobs[i].x.rows, BK));
+    const int64_t cs = std::min(chunk_steps, steps);
+    p.chunk = cs * BK;
+    p.splits = (int)cdiv(steps, cs);
+    p.slab_bytes = align_up((size_t)p.tiles * p.splits * TILE * TILE * sizeof(float), 256);
+  }
+}
+
+static bool valid_operand(const kfac_operand& o) {
+  if (o.cols < 0 || o.rows < 0 || (!o.ptr && o.rows > 0)) return false;
+  switch (o.layout) {
+    case KFAC_ROWMAJOR: return o.ld >= o.cols;
+    case KFAC_CHANNEL: return o.L > 0 && o.sB >= 0;
+    case KFAC_PATCH:
+      return o.L > 0 && o.C > 0 && o.H > 0 && o.W > 0 && o.kh > 0 && o.kw > 0 && o.sh > 0 &&
+             o.sw > 0 && o.ph >= 0 && o.pw >= 0 && o.Ho > 0 && o.Wo > 0 &&
+             (int64_t)o.Ho * o.Wo == o.L && o.cols == o.C * o.kh * o.kw && o.kh < 65536 &&
+             o.kw < 65536;
+    default: return false;
+  }
+}
+
+static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t ws_bytes,
+                        hipStream_t stream) {
+  Plan plans[MAXJ];
+  plan_jobs(jobs, njobs, plans);
+  FactorArgs args{};
+  args.njobs = njobs;
+  int tasks = 0, tiles = 0;
+  size_t off = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const kfac_factor_job& jb = jobs[i];
+    FactorJobDev& d = args.job[i];
+    d.x = to_dev(jb.x);
+    d.alpha = jb.alpha;
+    d.beta = jb.beta;
+    d.F = jb.F;
+    d.ldF = jb.ldF;
+    d.n = factor_n(jb);
+    d.t = (int)cdiv(d.n, TILE);
+    d.splits = plans[i].splits;
+    d.chunk = plans[i].chunk;
+    d.slab = reinterpret_cast<float*>(ws + off);
+    off += plans[i].slab_bytes;
+    d.task_begin = tasks;
+    d.tile_begin = tiles;
+    tasks += plans[i].tiles * plans[i].splits;
+    tiles += plans[i].tiles;
+    args.task_end[i] = tasks;
+    args.tile_end[i] = tiles;
+  }
+  if (off > ws_bytes) return KFAC_EWORKSPACE;
+  if (tasks == 0) return KFAC_OK;
+  {
+    ProfScope ps(KFAC_PROF_FACTOR_TILES, stream);
+    hipLaunchKernelGGL(kfac_factor_tiles, dim3(tasks), dim3(NTHREADS), 0, stream, args);
+  }
+  KFAC_CHECK_LAUNCH();
+  {
+    ProfScope ps(KFAC_PROF_FACTOR_REDUCE, stream);
+    hipLaunchKernelGGL(kfac_factor_reduce, dim3(tiles), dim3(NTHREADS), 0, stream, args);
+  }
+  KFAC_CHECK_LAUNCH();
+  return KFAC_OK;
+}
+
+static size_t group_ws(const kfac_factor_job* jobs, int njobs) {
+  Plan plans[MAXJ];
+  plan_jobs(jobs, njobs, plans);
+  size_t off = 0;
+  for (int i = 0; i < njobs; ++i) off += plans[i].slab_bytes;
+  return off;
+}
+
+}  // namespace kfac
+
+using namespace kfac;
+
+extern "C" size_t kfac_factor_workspace_bytes(const kfac_factor_job* jobs, int njobs) {
+  if (!jobs || njobs <= 0) return 0;
+  size_t m = 0;
+  for (int g = 0; g < njobs; g += MAXJ) m = std::max(m, group_ws(jobs + g, std::min(MAXJ, njobs - g)));
+  return m;
+}
+
+extern "C" int kfac_factor_update(const kfac_factor_job* jobs, int njobs, void* workspace,
+                                  size_t workspace_bytes, kfac_stream_t stream) {
+  if (njobs < 0 || (njobs > 0 && !jobs)) return KFAC_EINVAL;
+  for (int i = 0; i < njobs; ++i) {
+    const kfac_factor_job& j = jobs[i];
+    if (!valid_operand(j.x) || !j.F || j.ldF < factor_n(j)) return KFAC_EINVAL;
+    if ((int64_t)factor_n(j) > (int64_t)1 << 20) return KFAC_EINVAL;
+  }
+  // Groups run back to back on the stream, reusing the same workspace.
+  for (int g = 0; g < njobs; g += MAXJ) {
+    const int rc = factor_group(jobs + g, std::min(MAXJ, njobs - g), (char*)workspace,
+                                workspace_bytes, (hipStream_t)stream);
+    if (rc != KFAC_OK) return rc;
+  }
+  return KFAC_OK;
+}
+
+static kfac_operand rowmajor(const float* x, int64_t rows, int64_t cols, int64_t ld, int ones) {
+  kfac_operand o{};
+  o.ptr = x;
+  o.layout = KFAC_ROWMAJOR;
+  o.rows = rows;
+  o.cols = (int32_t)cols;
+  o.ld = ld;
+  o.has_ones = ones;
+  return o;
+}
+
+static int single(const kfac_operand& o, float alpha, float beta, float* F, int64_t ldF, void* ws,
+                  size_t wsb, kfac_stream_t s) {
+  kfac_factor_job j{};
+  j.x = o;
+  j.alpha = alpha;
+  j.beta = beta;
+  j.F = F;
+  j.ldF = ldF;
+  if (wsb < kfac_factor_workspace_bytes(&j, 1)) return KFAC_EWORKSPACE;
+  return kfac_factor_update(&j, 1, ws, wsb, s);
+}
+
+extern "C" int kfac_syrk_linear(const float* x, int64_t B, int64_t d, int64_t ldx, int has_ones,
+                                float alpha, float beta, float* F, int64_t ldF, void* ws,
+                                size_t wsb, kfac_stream_t s) {
+  return single(rowmajor(x, B, d, ldx, has_ones ? 1 : 0), alpha, beta, F, ldF, ws, wsb, s);
+}
+
+extern "C" int kfac_syrk_conv(const float* x, int64_t B, int C, int H, int W, int kh, int kw,
+                              int sh, int sw, int ph, int pw, int has_ones, float alpha, float beta,
+                              float* F, int64_t ldF, void* ws, size_t wsb, kfac_stream_t s) {
+  if (sh <= 0 || sw <= 0) return KFAC_EINVAL;
+  kfac_operand o{};
+  o.ptr = x;
+  o.layout = KFAC_PATCH;
+  o.C = C; o.H = H; o.W = W; o.kh = kh; o.kw = kw; o.sh = sh; o.sw = sw; o.ph = ph; o.pw = pw;
+  o.Ho = (H + 2 * ph - kh) / sh + 1;
+  o.Wo = (W + 2 * pw - kw) / sw + 1;
+  o.L = (int64_t)o.Ho * o.Wo;
+  o.sB = (int64_t)C * H * W;
+  o.rows = B * o.L;
+  o.cols = C * kh * kw;
+  o.has_ones = has_ones ? 1 : 0;
+  return single(o, alpha, beta, F, ldF, ws, wsb, s);
+}
+
+extern "C" int kfac_syrk_convgrad(const float* g, int64_t B, int C, int64_t L, float alpha,
+                                  float beta, float* F, int64_t ldF, void* ws, size_t wsb,
+                                  kfac_stream_t s) {
+  kfac_operand o{};
+  o.ptr = g;
+  o.layout = KFAC_CHANNEL;
+  o.L = L;
+  o.sB = (int64_t)C * L;
+  o.rows = B * L;
+  o.cols = C;
+  return single(o, alpha, beta, F, ldF, ws, wsb, s);
+}

@@ -1,0 +1,185 @@
+/*
+ * kfac_hip.h — C ABI of the MI355X (gfx950) KFAC curvature engine.
+ *
+ * Plain pointers and sizes only (no torch types): every buffer is device memory
+ * owned by the caller, every call is asynchronous on the given HIP stream
+ * (passed as an opaque `void*` = hipStream_t) and does no implicit sync, no
+ * allocation and no host<->device copy of data, so calls can be captured into a
+ * HIP graph.  Return value: 0 = launched, <0 = bad argument / launch failure
+ * (kfac_strerror).  Numerical failure (a non-positive pivot) is reported in a
+ * DEVICE int array `info`, LAPACK style, for the caller to read when it syncs.
+ *
+ * Each entry point names the reference interface it replaces
+ * (paths under TianmingQiu/BNN_KFAC).  The Python binding (ctypes) lives in
+ * bnn_kfac_amd/_native.py; INTEGRATION.md shows the binding a maintainer of the
+ * reference would add.
+ */
+#ifndef KFAC_HIP_H
+#define KFAC_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__) || defined(__clang__)
+#define KFAC_API __attribute__((visibility("default")))
+#else
+#define KFAC_API
+#endif
+
+typedef void* kfac_stream_t; /* hipStream_t */
+
+enum kfac_status {
+  KFAC_OK = 0,
+  KFAC_EINVAL = -1,     /* bad argument (null pointer, bad shape, bad layout) */
+  KFAC_ELAUNCH = -2,    /* a HIP launch failed */
+  KFAC_EWORKSPACE = -3, /* workspace too small */
+};
+
+/* ------------------------------------------------------------------ factors
+ * F = beta * F + alpha * X~^T X~, X~ = [X | 1] (ones column iff has_ones),
+ * X the (rows x cols) input whose element (k, i) is addressed per `layout`:
+ *   KFAC_ROWMAJOR: ptr[k*ld + i]                     (Linear a, Linear g_rec)
+ *   KFAC_CHANNEL : ptr[(k/L)*sB + (k%L) + i*L]        (Conv2d g_rec (B,C,Ho*Wo))
+ *   KFAC_PATCH   : implicit im2col of x (B,C,H,W):   k = b*L + oh*Wo + ow,
+ *                  i = c*kh*kw + ki*kw + kj  ->  x[b, c, oh*sh+ki-ph, ow*sw+kj-pw]
+ *                  (0 outside the image)           (Conv2d a, F.unfold order)
+ * F is n x n row-major with n = cols + has_ones, written exactly symmetric.
+ * Replaces models/curvatures.py:341-363 (unfold/permute + the two torch.mm
+ * calls + the per-batch-mean `/ float(cols)` + the `+=` accumulation).     */
+enum kfac_layout { KFAC_ROWMAJOR = 0, KFAC_CHANNEL = 1, KFAC_PATCH = 2 };
+
+typedef struct kfac_operand {
+  const float* ptr;
+  int32_t layout;
+  int32_t cols;
+  int64_t rows;
+  int32_t has_ones;
+  int32_t reserved0;
+  int64_t ld;  /* ROWMAJOR row stride (elements) */
+  int64_t L;   /* CHANNEL/PATCH: positions per sample (Ho*Wo) */
+  int64_t sB;  /* CHANNEL/PATCH: sample stride (elements) */
+  int32_t C, H, W, kh, kw, sh, sw, ph, pw, Ho, Wo, reserved1; /* PATCH geometry */
+} kfac_operand;
+
+typedef struct kfac_factor_job {
+  kfac_operand x;
+  float alpha; /* 1/cols = per-batch mean (curvatures.py:349,356); 1/B_global when sharded */
+  float beta;  /* 0 = first update assigns, 1 = later updates add (curvatures.py:359-363) */
+  float* F;
+  int64_t ldF;
+} kfac_factor_job;
+
+/* Workspace (split-K slabs) needed by kfac_factor_update for these jobs. */
+KFAC_API size_t kfac_factor_workspace_bytes(const kfac_factor_job* jobs, int njobs);
+/* All jobs of one KFAC.update() in one grouped MFMA launch + one reduce launch.
+ * Replaces KFAC.update, models/curvatures.py:325-365. */
+KFAC_API int kfac_factor_update(const kfac_factor_job* jobs, int njobs, void* workspace,
+                       size_t workspace_bytes, kfac_stream_t stream);
+
+/* Single-factor conveniences (same kernels). */
+KFAC_API int kfac_syrk_linear(const float* x, int64_t B, int64_t d, int64_t ldx, int has_ones,
+                     float alpha, float beta, float* F, int64_t ldF, void* workspace,
+                     size_t workspace_bytes, kfac_stream_t stream);
+KFAC_API int kfac_syrk_conv(const float* x, int64_t B, int C, int H, int W, int kh, int kw, int sh,
+                   int sw, int ph, int pw, int has_ones, float alpha, float beta, float* F,
+                   int64_t ldF, void* workspace, size_t workspace_bytes, kfac_stream_t stream);
+KFAC_API int kfac_syrk_convgrad(const float* g, int64_t B, int C, int64_t L, float alpha, float beta,
+                       float* F, int64_t ldF, void* workspace, size_t workspace_bytes,
+                       kfac_stream_t stream);
+
+/* ---------------------------------------------------------------- inversion
+ * R = scale * (F + F^T)/2 + shift * I, computed in fp64 on the device, then
+ *   KFAC_OUT_INV_CHOL: out = L, lower, L L^T = R^{-1}   (= cholesky(inverse(R)))
+ *   KFAC_OUT_INVERSE : out = R^{-1} (full, symmetric)
+ * via C = chol(P R P) (P the exchange matrix), X = C^{-1}, L = P X^T P.
+ * KFAC.invert passes scale = sqrt(multiply), shift = sqrt(add)
+ * (models/curvatures.py:367-398); the regression block passes scale = N,
+ * shift = N*tau with KFAC_OUT_INVERSE (regression_ll_block.py:130-133).
+ * info[j] (device) = 0, or the 1-based index of the first non-positive pivot
+ * of job j (the reference's RuntimeError / LinAlgError condition).          */
+enum kfac_inv_out { KFAC_OUT_INV_CHOL = 0, KFAC_OUT_INVERSE = 1 };
+
+typedef struct kfac_invert_job {
+  const float* F;
+  int64_t ldF;
+  int32_t n;
+  int32_t out_kind;
+  double scale;
+  double shift;
+  float* out;
+  int64_t ldo;
+} kfac_invert_job;
+
+KFAC_API size_t kfac_invert_workspace_bytes(const kfac_invert_job* jobs, int njobs);
+KFAC_API int kfac_invert(const kfac_invert_job* jobs, int njobs, void* workspace, size_t workspace_bytes,
+                int32_t* info, kfac_stream_t stream);
+/* Single-factor convenience: KFAC.invert for one factor. */
+KFAC_API int kfac_damped_inv_chol(const float* F, int n, int64_t ldF, double sqrt_s, double sqrt_n,
+                         float* L, int64_t ldL, void* workspace, size_t workspace_bytes,
+                         int32_t* info, kfac_stream_t stream);
+
+/* ------------------------------------------------------------ eigenvalues
+ * Symmetric eigendecomposition of (F + F^T)/2 (fp64 on device): evals ascending
+ * (torch.symeig / eigvalsh order), evecs (optional, may be NULL) as columns,
+ * row-major n x n fp32.  Replaces models/utilities.py:120-159.           */
+typedef struct kfac_eig_job {
+  const float* F;
+  int64_t ldF;
+  int32_t n;
+  int32_t reserved;
+  double* evals;
+  float* evecs;
+  int64_t ldv;
+} kfac_eig_job;
+
+KFAC_API size_t kfac_eig_workspace_bytes(const kfac_eig_job* jobs, int njobs);
+KFAC_API int kfac_syev(const kfac_eig_job* jobs, int njobs, void* workspace, size_t workspace_bytes,
+              int32_t* info, kfac_stream_t stream);
+
+/* ------------------------------------------------- predictive variance
+ * v[j][b] = J_jb kron(K1_j, K2_j) J_jb^T without forming the Kronecker product:
+ * with M = J_jb viewed (nA x nG) row-major (the reference's flat order
+ * a*nG + g), v = <K1^T M, M K2^T>_F.  K1/K2 may be flagged lower-triangular
+ * (Cholesky factors) to skip their zero blocks.
+ * out[b] = sum_j |v[j][b]| if abs_sum else sum_j v[j][b].
+ * Replaces classification_ll_block.py:126-132 (torch.kron + J H J^T) and
+ * regression_ll_block.py:128-139 (kronecker_product + J H J^T).          */
+typedef struct kfac_quad_job {
+  const float* J;
+  int64_t ldJ; /* stride between the nb rows of J (elements) */
+  int32_t nA, nG;
+  const float* K1;
+  int64_t ld1;
+  const float* K2;
+  int64_t ld2;
+  int32_t lower1, lower2;
+  float* v; /* optional (may be NULL): nb raw values for this job */
+} kfac_quad_job;
+
+KFAC_API size_t kfac_quadform_workspace_bytes(const kfac_quad_job* jobs, int njobs, int64_t nb);
+KFAC_API int kfac_kron_quadform(const kfac_quad_job* jobs, int njobs, int64_t nb, int abs_sum, float* out,
+                       void* workspace, size_t workspace_bytes, kfac_stream_t stream);
+
+/* -------------------------------------------------------------- profiling
+ * Optional HIP-event timing of the library's own launches, recorded on the
+ * stream each kernel is launched on (off by default; not graph-capturable when
+ * on).  Kernel ids: 0 factor tiles (MFMA SYRK), 1 factor reduce, 2 whole invert
+ * call, 3 quadform tiles.  kfac_profile_read syncs the recorded events.     */
+enum kfac_prof_id { KFAC_PROF_FACTOR_TILES = 0, KFAC_PROF_FACTOR_REDUCE = 1, KFAC_PROF_INVERT = 2,
+                    KFAC_PROF_QUAD_TILES = 3, KFAC_PROF_COUNT = 4 };
+KFAC_API int kfac_profile_enable(int on);
+KFAC_API int kfac_profile_read(int id, double* total_ms, int64_t* launches);
+KFAC_API int kfac_profile_reset(void);
+
+/* ------------------------------------------------------------------- misc */
+KFAC_API const char* kfac_strerror(int status);
+KFAC_API const char* kfac_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KFAC_HIP_H */

@@ -1,0 +1,115 @@
+"""GPU parity: eigenvalues (get_eigenvalues) and the Kronecker predictive variance."""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from conftest import golden
+from oracle import kfac_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(x, dev):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+
+
+def test_get_eigenvalues_golden(hip_device):
+    from bnn_kfac_amd.utilities import get_eigenvalues
+    g = golden("g1_small_linear.npz")
+    factors = [[_t(g["A0"], hip_device), _t(g["G0"], hip_device)],
+               [_t(g["A1"], hip_device), _t(g["G1"], hip_device)]]
+    ev = get_eigenvalues(factors).cpu().numpy()
+    np.testing.assert_allclose(ev, g["eigvals"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(ev, O.get_eigenvalues([(g["A0"], g["G0"]), (g["A1"], g["G1"])]),
+                               rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 64, 127, 128])
+def test_eigvecs_orthonormal(hip_device, n):
+    from bnn_kfac_amd.utilities import symeig
+    rng = np.random.default_rng(n)
+    X = rng.standard_normal((n, n)).astype(np.float32)
+    F = (X + X.T).astype(np.float32)
+    (ev, V), = symeig([_t(F, hip_device)], eigenvectors=True)
+    ev, V = ev.cpu().numpy(), V.cpu().numpy().astype(np.float64)
+    np.testing.assert_allclose(ev, np.linalg.eigvalsh(F.astype(np.float64)), rtol=1e-6,
+                               atol=1e-9 * np.abs(ev).max())
+    np.testing.assert_allclose(V.T @ V, np.eye(n), atol=1e-5)
+    np.testing.assert_allclose(F @ V, V * ev, atol=1e-4 * np.abs(ev).max())
+
+
+def test_quadform_vs_dense_reference_route(hip_device):
+    from bnn_kfac_amd.variance import kron_quadform
+    rng = np.random.default_rng(0)
+    for nA, nG, nb in [(5, 3, 1), (27, 6, 4), (129, 10, 3), (70, 65, 2)]:
+        K1 = np.tril(rng.standard_normal((nA, nA))).astype(np.float32)
+        K2 = np.tril(rng.standard_normal((nG, nG))).astype(np.float32)
+        J = rng.standard_normal((nb, nA * nG)).astype(np.float32)
+        out, v = kron_quadform([(_t(J, hip_device), _t(K1, hip_device), _t(K2, hip_device))],
+                               lower=True, per_term=True)
+        ref = O.kron_quadform_dense(J, K1, K2)
+        np.testing.assert_allclose(v.cpu().numpy()[0], ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max())
+        np.testing.assert_allclose(out.cpu().numpy(), np.abs(ref), rtol=1e-4,
+                                   atol=1e-4 * np.abs(ref).max())
+
+
+def test_quadform_mlp_layer1_vec_trick(hip_device):
+    """MLP layer-1 shape (785 x 128): the reference's kron would be 40 GB."""
+    from bnn_kfac_amd.variance import kron_quadform
+    rng = np.random.default_rng(1)
+    nA, nG, nb = 785, 128, 3
+    K1 = np.tril(rng.standard_normal((nA, nA)) * 0.1).astype(np.float32)
+    K2 = np.tril(rng.standard_normal((nG, nG)) * 0.1).astype(np.float32)
+    J = rng.standard_normal((nb, nA * nG)).astype(np.float32)
+    out, v = kron_quadform([(_t(J, hip_device), _t(K1, hip_device), _t(K2, hip_device))], per_term=True)
+    ref = O.kron_quadform(J, K1, K2)
+    np.testing.assert_allclose(v.cpu().numpy()[0], ref, rtol=1e-4, atol=1e-5 * np.abs(ref).max())
+
+
+def test_classification_variance_golden(hip_device):
+    """G6: the reference's per-batch pred_std / entropy on BaseNet_750 (batch 1 and 8)."""
+    from bnn_kfac_amd.variance import kron_quadform, layer_jacobian
+    from models_for_tests import BaseNet750
+    g = golden("g5_basenet750.npz")
+    net = BaseNet750()
+    net.load_state_dict({k[2:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("w_")})
+    net = net.to(hip_device)
+    layers = [net.conv1, net.conv2, net.fc1]
+    for tag in ("b1", "b8"):
+        x = _t(g[f"var_{tag}_x"], hip_device)
+        pred = torch.softmax(net(x), dim=1)
+        idx = np.argmax(pred.detach().cpu().numpy(), axis=1)
+        go = torch.zeros_like(pred)
+        go[:, idx] = 1
+        terms = []
+        for li, layer in enumerate(layers):
+            J = layer_jacobian(pred, layer, go)
+            np.testing.assert_allclose(J.detach().cpu().numpy(), g[f"var_{tag}_J{li}"], rtol=1e-4,
+                                       atol=1e-6)
+            terms.append((J, _t(g[f"LA{li}"], hip_device), _t(g[f"LG{li}"], hip_device)))
+        out, v = kron_quadform(terms, per_term=True)
+        np.testing.assert_allclose(v.cpu().numpy()[:, 0], g[f"var_{tag}_v"], rtol=1e-4, atol=1e-9)
+        np.testing.assert_allclose(float(out[0]), g[f"var_{tag}_std"], rtol=1e-4)
+        ent = 0.5 * np.log2(2 * np.e * np.pi * float(out[0]))
+        np.testing.assert_allclose(ent, g[f"var_{tag}_entropy"], rtol=1e-4, atol=1e-5)
+
+
+def test_regression_variance_golden(hip_device):
+    """G7: regression block, pinv(N(q + tau I)) (x) pinv(N(h + tau I)) on device."""
+    from bnn_kfac_amd.curvatures import KFAC
+    from bnn_kfac_amd.variance import kron_quadform, regression_inverse_factors
+    g = golden("g7_regression.npz")
+    net = nn.Sequential(nn.Linear(1, 30), nn.ReLU(), nn.Linear(30, 30), nn.ReLU(),
+                        nn.Linear(30, 1)).to(hip_device)
+    kfac = KFAC(net)
+    layers = [net[0], net[2], net[4]]
+    for li, layer in enumerate(layers):
+        kfac.state[layer] = [_t(g[f"q{li}"], hip_device), _t(g[f"h{li}"], hip_device)]
+    N, tau, sigma = float(g["N"]), float(g["tau"]), float(g["sigma"])
+    inv = regression_inverse_factors(kfac, N, tau)
+    for j in range(len(g["xs"])):
+        terms = [(_t(g[f"J_{j}_{li}"], hip_device), inv[li][0], inv[li][1]) for li in range(3)]
+        out, v = kron_quadform(terms, lower=False, per_term=True)
+        np.testing.assert_allclose(v.cpu().numpy()[:, 0], g["v"][j], rtol=2e-3, atol=1e-7)
+        np.testing.assert_allclose(float(out[0]) ** 0.5 + sigma, g["std"][j], rtol=1e-4)

@@ -1,0 +1,195 @@
+"""GPU parity: factor accumulation (KFAC.update) through libkfac_hip vs the oracle.
+
+Tolerances: factors are fp32 sums of products; the kernel's fp32 MFMA chain and the
+reference's MKL sgemm each sit ~1e-7 relative from the fp64 truth, so the
+criterion is rtol 1e-5 against the fp64 oracle and the goldens.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from conftest import golden
+from oracle import kfac_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+FT = dict(rtol=1e-5, atol=1e-6)
+
+
+def _t(x, dev):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+
+
+def test_mfma_layout_asymmetric(hip_device):
+    """Raw C-ABI, one asymmetric operand: catches row/col swaps in the MFMA C-layout."""
+    from bnn_kfac_amd import _native as N
+    rng = np.random.default_rng(0)
+    for B, d, ones in [(33, 70, True), (1, 1, False), (64, 64, True), (97, 129, False), (300, 10, True)]:
+        x = rng.integers(-3, 4, size=(B, d)).astype(np.float32)  # exact small integers
+        F = torch.full((d + ones, d + ones), np.nan, device=hip_device)
+        N.factor_update([N.factor_job(N.rowmajor_operand(_t(x, hip_device), ones), F, 1.0, 0.0)],
+                        hip_device)
+        xo = np.concatenate([x, np.ones((B, 1), np.float32)], 1) if ones else x
+        np.testing.assert_array_equal(F.cpu().numpy(), xo.T.astype(np.float64) @ xo)
+
+
+def test_strided_rows_and_beta(hip_device):
+    from bnn_kfac_amd import _native as N
+    rng = np.random.default_rng(1)
+    base = rng.standard_normal((200, 96)).astype(np.float32)
+    xt = _t(base, hip_device)[:, 5:85]  # ld 96, cols 80
+    F0 = rng.standard_normal((81, 81)).astype(np.float32)
+    F0 = F0 + F0.T
+    F = _t(F0, hip_device)
+    N.factor_update([N.factor_job(N.rowmajor_operand(xt, True), F, 0.25, 1.0)], hip_device)
+    x = base[:, 5:85].astype(np.float64)
+    xo = np.concatenate([x, np.ones((200, 1))], 1)
+    want = F0 + 0.25 * xo.T @ xo
+    # F0 + x^T x cancels to near zero in places: absolute tolerance at the sum's scale
+    np.testing.assert_allclose(F.cpu().numpy(), want, rtol=1e-5, atol=1e-6 * np.abs(0.25 * xo.T @ xo).max())
+
+
+def test_small_linear_golden(hip_device):
+    from bnn_kfac_amd.curvatures import KFAC
+    g = golden("g1_small_linear.npz")
+    net = nn.Sequential(nn.Linear(20, 12), nn.ReLU(), nn.Linear(12, 5, bias=False)).to(hip_device)
+    kfac = KFAC(net)
+    for bi in range(3):
+        kfac.record[net[0]] = [_t(g[f"b{bi}_a1"], hip_device), _t(g[f"b{bi}_g1"], hip_device)]
+        kfac.record[net[2]] = [_t(g[f"b{bi}_a2"], hip_device), _t(g[f"b{bi}_g2"], hip_device)]
+        kfac.update(batch_size=len(g[f"b{bi}_a1"]))
+    assert list(kfac.state.keys()) == [net[0], net[2]]
+    for li, layer in enumerate([net[0], net[2]]):
+        A, G = kfac.state[layer]
+        np.testing.assert_allclose(A.cpu().numpy(), g[f"A{li}"], **FT)
+        np.testing.assert_allclose(G.cpu().numpy(), g[f"G{li}"], **FT)
+        assert torch.equal(A, A.t()) and torch.equal(G, G.t())
+
+
+def mlp_batches(seed=123, sizes=(256, 256, 256, 96)):
+    rng = np.random.default_rng(seed)
+    for B in sizes:
+        yield (B, rng.random((B, 784), dtype=np.float32), rng.standard_normal((B, 128), dtype=np.float32),
+               rng.random((B, 128), dtype=np.float32), rng.standard_normal((B, 10), dtype=np.float32))
+
+
+def test_mlp_golden_and_oracle(hip_device):
+    from bnn_kfac_amd.curvatures import KFAC
+    g = golden("g1_mlp.npz")
+    net = nn.Sequential(nn.Linear(784, 128), nn.ReLU(), nn.Linear(128, 10)).to(hip_device)
+    kfac = KFAC(net)
+    ref = O.OracleKFAC(np.float64)
+    for B, a1, g1, a2, g2 in mlp_batches():
+        kfac.record[net[0]] = [_t(a1, hip_device), _t(g1, hip_device)]
+        kfac.record[net[2]] = [_t(a2, hip_device), _t(g2, hip_device)]
+        kfac.update(batch_size=B)
+        ref.update_linear("fc1", a1, g1, True)
+        ref.update_linear("fc2", a2, g2, True)
+    A1, G1 = [t.cpu().numpy() for t in kfac.state[net[0]]]
+    A2, G2 = [t.cpu().numpy() for t in kfac.state[net[2]]]
+    np.testing.assert_allclose(A1, ref.state["fc1"][0], **FT)
+    np.testing.assert_allclose(G1, ref.state["fc1"][1], **FT)
+    np.testing.assert_allclose(A2, ref.state["fc2"][0], **FT)
+    np.testing.assert_allclose(G2, ref.state["fc2"][1], **FT)
+    np.testing.assert_allclose(np.diag(A1), g["A1_diag"], **FT)
+    np.testing.assert_allclose(A1[:8], g["A1_head"], **FT)
+    np.testing.assert_allclose(A1[-8:], g["A1_tail"], **FT)
+    np.testing.assert_allclose(G1, g["G1"], **FT)
+    np.testing.assert_allclose(A2, g["A2"], **FT)
+    np.testing.assert_allclose(G2, g["G2"], **FT)
+
+
+def test_conv_golden(hip_device):
+    from bnn_kfac_amd.curvatures import KFAC
+    g = golden("g4_conv.npz")
+    convs = []
+    for li in range(4):
+        kh, kw, sh, sw, ph, pw, bias, cout = [int(v) for v in g[f"meta{li}"]]
+        cin = g[f"x{li}"].shape[1]
+        convs.append(nn.Conv2d(cin, cout, (kh, kw), stride=(sh, sw), padding=(ph, pw), bias=bool(bias)))
+    net = nn.Sequential(*convs).to(hip_device)
+    kfac = KFAC(net)
+    for _ in range(2):
+        for li, layer in enumerate(convs):
+            kfac.record[layer] = [_t(g[f"x{li}"], hip_device), _t(g[f"g{li}"], hip_device)]
+        kfac.update(batch_size=0)
+    for li, layer in enumerate(convs):
+        A, G = kfac.state[layer]
+        np.testing.assert_allclose(A.cpu().numpy(), g[f"A{li}"], **FT)
+        np.testing.assert_allclose(G.cpu().numpy(), g[f"G{li}"], **FT)
+
+
+@pytest.mark.parametrize("spec", [
+    # (B, Cin, H, W, Cout, k, stride, pad, bias): LeNet-5 / BaseNet_15k shapes + odd ones
+    (16, 1, 28, 28, 6, (5, 5), (1, 1), (2, 2), True),
+    (16, 6, 14, 14, 16, (5, 5), (1, 1), (0, 0), True),
+    (8, 5, 12, 12, 10, (5, 5), (1, 1), (0, 0), True),
+    (3, 7, 9, 11, 70, (3, 2), (2, 3), (1, 0), False),
+    (2, 13, 6, 6, 3, (1, 1), (1, 1), (0, 0), True),
+])
+def test_conv_shapes_vs_oracle(hip_device, spec):
+    from bnn_kfac_amd.curvatures import KFAC
+    B, Cin, H, W, Cout, k, s, p, bias = spec
+    rng = np.random.default_rng(sum(spec[:5]))
+    conv = nn.Conv2d(Cin, Cout, k, stride=s, padding=p, bias=bias).to(hip_device)
+    x = rng.random((B, Cin, H, W), dtype=np.float32)
+    Ho, Wo = (H + 2 * p[0] - k[0]) // s[0] + 1, (W + 2 * p[1] - k[1]) // s[1] + 1
+    gr = rng.standard_normal((B, Cout, Ho, Wo), dtype=np.float32)
+    kfac = KFAC(conv)
+    kfac.record[conv] = [_t(x, hip_device), _t(gr, hip_device)]
+    kfac.update(batch_size=B)
+    A, G = kfac.state[conv]
+    np.testing.assert_allclose(A.cpu().numpy(), O.conv_factor_A(x, k, p, s, bias, np.float64), **FT)
+    np.testing.assert_allclose(G.cpu().numpy(), O.grad_factor(gr, np.float64), **FT)
+
+
+def test_hooks_end_to_end_basenet750(hip_device):
+    """Full forward/backward through the hooks reproduces the reference's factors (G5)."""
+    from bnn_kfac_amd.curvatures import KFAC
+    from models_for_tests import BaseNet750
+    g = golden("g5_basenet750.npz")
+    net = BaseNet750()
+    net.load_state_dict({k[2:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("w_")})
+    net = net.to(hip_device)
+    kfac = KFAC(net)
+    crit = nn.CrossEntropyLoss()
+    for bi in range(2):
+        x = _t(g[f"x{bi}"], hip_device)
+        y = torch.from_numpy(g[f"y{bi}"]).to(hip_device)
+        loss = crit(net(x), y)
+        net.zero_grad()
+        loss.backward()
+        kfac.update(batch_size=8)
+    for li, layer in enumerate([net.conv1, net.conv2, net.fc1]):
+        A, G = kfac.state[layer]
+        np.testing.assert_allclose(A.cpu().numpy(), g[f"A{li}"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(G.cpu().numpy(), g[f"G{li}"], rtol=1e-4, atol=1e-6)
+
+
+def test_deterministic_and_large_batch(hip_device):
+    """Bitwise-reproducible (no atomics) and right at B = 4096 (the bench shape)."""
+    from bnn_kfac_amd.curvatures import KFAC
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Linear(784, 128), nn.ReLU(), nn.Linear(128, 10)).to(hip_device)
+    a1 = torch.rand(4096, 784, device=hip_device)
+    g1 = torch.randn(4096, 128, device=hip_device)
+    outs = []
+    for _ in range(2):
+        kfac = KFAC(net)
+        kfac.record[net[0]] = [a1, g1]
+        kfac.record[net[2]] = [a1[:, :128], g1[:, :10]]
+        kfac.update(4096)
+        outs.append([t.clone() for t in kfac.state[net[0]]])
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    ref = O.linear_factor_A(a1.cpu().numpy(), True, np.float64)
+    np.testing.assert_allclose(outs[0][0].cpu().numpy(), ref, **FT)
+
+
+def test_empty_batch_rows(hip_device):
+    """A zero-row operand contributes exactly nothing and reads nothing."""
+    from bnn_kfac_amd import _native as N
+    x = torch.empty(0, 5, device=hip_device)
+    F = torch.zeros(6, 6, device=hip_device)
+    N.factor_update([N.factor_job(N.rowmajor_operand(x, True), F, 1.0, 1.0)], hip_device)
+    assert torch.equal(F, torch.zeros_like(F))

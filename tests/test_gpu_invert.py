@@ -1,0 +1,139 @@
+"""GPU parity: KFAC.invert (fp64 device potrf + trtri) vs the fp64 oracle and the goldens.
+
+Criterion: the device result within rtol 1e-4 of the fp64
+restatement cholesky(inverse(sqrt(s) F + sqrt(n) I)); against the reference's own
+fp32 output only to the reference's own error (it is ~5e-3 off at cond 5e4).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from conftest import golden
+from oracle import kfac_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(x, dev):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+
+
+def _spd(n, rng, cond=1e4):
+    q, _ = np.linalg.qr(rng.standard_normal((n, n)))
+    ev = np.logspace(0, np.log10(cond), n)
+    return ((q * ev) @ q.T).astype(np.float32)
+
+
+@pytest.mark.parametrize("n", [1, 5, 63, 64, 65, 128, 129, 200, 785])
+def test_inv_chol_sizes_vs_fp64(hip_device, n):
+    from bnn_kfac_amd import _native as N
+    rng = np.random.default_rng(n)
+    F = _spd(n, rng)
+    Ft = _t(F, hip_device)
+    L = torch.empty_like(Ft)
+    info = N.invert([N.invert_job(Ft, L, 200 ** 0.5, 0.04 ** 0.5)], hip_device)
+    assert int(info.cpu()[0]) == 0
+    ref = O.invert_factor(F, 0.04, 200)
+    got = L.cpu().numpy()
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-7 * np.abs(ref).max())
+    assert np.all(np.triu(got, 1) == 0)
+
+
+def test_grouped_invert_and_inverse_kind(hip_device):
+    from bnn_kfac_amd import _native as N
+    rng = np.random.default_rng(3)
+    mats = [_spd(n, rng, 1e3) for n in (10, 129, 70, 300)]
+    jobs, outs = [], []
+    for i, F in enumerate(mats):
+        Ft = _t(F, hip_device)
+        out = torch.empty_like(Ft)
+        kind = N.OUT_INVERSE if i % 2 else N.OUT_INV_CHOL
+        jobs.append(N.invert_job(Ft, out, 3.0, 0.5, kind))
+        outs.append((Ft, out, kind))
+    info = N.invert(jobs, hip_device)
+    assert not info.cpu().any()
+    for F, (_, out, kind) in zip(mats, outs):
+        R = O.damped_factor(F, 0.25, 9.0)
+        ref = np.linalg.inv(R) if kind == N.OUT_INVERSE else np.linalg.cholesky(np.linalg.inv(R))
+        np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-4, atol=1e-7 * np.abs(ref).max())
+
+
+def test_kfac_invert_small_golden(hip_device):
+    from bnn_kfac_amd.curvatures import KFAC
+    g = golden("g1_small_linear.npz")
+    net = nn.Sequential(nn.Linear(20, 12), nn.ReLU(), nn.Linear(12, 5, bias=False)).to(hip_device)
+    kfac = KFAC(net)
+    for bi in range(3):
+        kfac.record[net[0]] = [_t(g[f"b{bi}_a1"], hip_device), _t(g[f"b{bi}_g1"], hip_device)]
+        kfac.record[net[2]] = [_t(g[f"b{bi}_a2"], hip_device), _t(g[f"b{bi}_g2"], hip_device)]
+        kfac.update(batch_size=16)
+    for tag, (add, mult) in {"s": (0.2 ** 2, 200), "t": (1, 200),
+                             "l": ([0.1, 0.3], [10.0, 20.0])}.items():
+        kfac.invert(add, mult)
+        pairs = O.damping_pairs(add, mult, 2)
+        for li, layer in enumerate([net[0], net[2]]):
+            LA, LG = [t.cpu().numpy() for t in kfac.inv_state[layer]]
+            A, G = [t.cpu().numpy() for t in kfac.state[layer]]
+            n, s = pairs[li]
+            np.testing.assert_allclose(LA, O.invert_factor(A, n, s), rtol=1e-4, atol=1e-8)
+            np.testing.assert_allclose(LG, O.invert_factor(G, n, s), rtol=1e-4, atol=1e-8)
+            np.testing.assert_allclose(LA, g[f"inv{tag}_LA{li}"], rtol=2e-4, atol=2e-5)
+            np.testing.assert_allclose(LG, g[f"inv{tag}_LG{li}"], rtol=2e-4, atol=2e-5)
+
+
+def test_kfac_invert_mlp_golden(hip_device):
+    from bnn_kfac_amd.curvatures import KFAC
+    g = golden("g1_mlp.npz")
+    net = nn.Sequential(nn.Linear(784, 128), nn.ReLU(), nn.Linear(128, 10)).to(hip_device)
+    kfac = KFAC(net)
+    rng = np.random.default_rng(123)
+    for B in (256, 256, 256, 96):
+        a1 = rng.random((B, 784), dtype=np.float32)
+        g1 = rng.standard_normal((B, 128), dtype=np.float32)
+        a2 = rng.random((B, 128), dtype=np.float32)
+        g2 = rng.standard_normal((B, 10), dtype=np.float32)
+        kfac.record[net[0]] = [_t(a1, hip_device), _t(g1, hip_device)]
+        kfac.record[net[2]] = [_t(a2, hip_device), _t(g2, hip_device)]
+        kfac.update(B)
+    kfac.invert(0.2 ** 2, 200)
+    LA1, LG1 = [t.cpu().numpy() for t in kfac.inv_state[net[0]]]
+    LA2, LG2 = [t.cpu().numpy() for t in kfac.inv_state[net[2]]]
+    A1 = kfac.state[net[0]][0].cpu().numpy()
+    # against fp64 truth on the device's own factor: tight
+    np.testing.assert_allclose(LA1, O.invert_factor(A1, 0.04, 200), rtol=1e-4, atol=1e-7)
+    # against the reference's fp32 outputs: the reference's own error band
+    np.testing.assert_allclose(LG1, g["LG1"], rtol=5e-4, atol=1e-5)
+    np.testing.assert_allclose(LA2, g["LA2"], rtol=5e-4, atol=1e-5)
+    np.testing.assert_allclose(LG2, g["LG2"], rtol=5e-4, atol=1e-5)
+    np.testing.assert_allclose(np.diag(LA1), g["LA1_diag"], rtol=1e-2, atol=1e-5)
+    np.testing.assert_allclose(LA1[-8:], g["LA1_tail"], rtol=1e-2, atol=2e-3)
+
+
+def test_singular_raises_linalgerror(hip_device):
+    from bnn_kfac_amd.curvatures import KFAC
+    g = golden("g2_singular.npz")
+    assert str(g["outcome"]) == "LinAlgError"
+    net = nn.Sequential(nn.Linear(6, 4)).to(hip_device)
+    kfac = KFAC(net)
+    kfac.record[net[0]] = [_t(g["a"], hip_device), _t(g["g"], hip_device)]
+    kfac.update(2)
+    with pytest.raises(np.linalg.LinAlgError):
+        kfac.invert(0.0, 1.0)
+
+
+def test_invert_identity_property_wide(hip_device):
+    """Size-independent check at a wide-MLP-like size: L L^T R = I."""
+    from bnn_kfac_amd import _native as N
+    rng = np.random.default_rng(9)
+    n = 1500
+    X = rng.random((4096, n), dtype=np.float32)
+    Xt = _t(X, hip_device)
+    F = (Xt.t() @ Xt) / 4096
+    L = torch.empty_like(F)
+    info = N.invert([N.invert_job(F, L, 200 ** 0.5, 0.04 ** 0.5)], hip_device)
+    assert int(info.cpu()[0]) == 0
+    R = O.damped_factor(F.cpu().numpy(), 0.04, 200)
+    Ld = L.cpu().numpy().astype(np.float64)
+    E = Ld.T @ R @ Ld  # = I for the exact factor (L^T R L = I  <=>  L L^T = R^{-1})
+    assert np.abs(E - np.eye(n)).max() < 1e-3
