@@ -159,23 +159,28 @@ def main():
     for _ in range(args.warmup):
         one_pass()
     sync()
-    N.profile_reset()
-    N.profile_enable(True)
-    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_pass()
     sync()
     elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    # Kernel durations: the same K steps again with the library's HIP-event timing
+    # on (events recorded around each launch, on its stream).  Kept out of the timed
+    # region above because the event packets add ~10 us per launch boundary.
+    N.profile_reset()
+    N.profile_enable(True)
+    for _ in range(args.steps):
+        one_pass()
+    sync()
     N.profile_enable(False)
     tiles_ms, tiles_n = N.profile_read(N.PROF_FACTOR_TILES)
     red_ms, red_n = N.profile_read(N.PROF_FACTOR_REDUCE)
     inv_ms, inv_n = N.profile_read(N.PROF_INVERT)
     N.profile_reset()
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
 
     images_total = world * args.images * args.steps
     value = images_total / elapsed

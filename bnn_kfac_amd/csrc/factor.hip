@@ -72,45 +72,60 @@ __global__ __launch_bounds__(NTHREADS) void kfac_factor_tiles(FactorArgs args) {
   }
 }
 
+// One block = one 16-row strip of one 64x64 tile: float4 slab reads (all splits
+// in flight at once), F = beta*F + alpha*sum, then the mirrored strip through LDS.
 __global__ __launch_bounds__(NTHREADS) void kfac_factor_reduce(FactorArgs args) {
-  __shared__ float tileT[TILE * LDP];
-  const int gtile = blockIdx.x;
+  __shared__ float strip[16 * LDP];
+  const int gtile = blockIdx.x >> 2, s0 = (blockIdx.x & 3) * 16;
   int j = 0;
   while (j + 1 < args.njobs && gtile >= args.tile_end[j]) ++j;
   const FactorJobDev& J = args.job[j];
   const int tile = gtile - J.tile_begin;
   int ti, tj;
   tri_decode(tile, ti, tj);
-  const int i0 = ti * TILE, j0 = tj * TILE;
+  const int i0 = ti * TILE, j0 = tj * TILE, n = J.n;
   const bool diag = ti == tj;
-  const float* slab = J.slab + (size_t)tile * J.splits * TILE * TILE;
-  const float alpha = J.alpha, beta = J.beta;
-  for (int e = threadIdx.x; e < TILE * TILE; e += NTHREADS) {
-    const int r = e >> 6, c = e & 63;
-    const int gi = i0 + r, gj = j0 + c;
-    if (gi >= J.n || gj >= J.n || (diag && c > r)) continue;
-    float s = 0.f;
-    for (int sp = 0; sp < J.splits; ++sp) s += slab[(size_t)sp * TILE * TILE + e];
-    float* f = J.F + (int64_t)gi * J.ldF + gj;
-    const float val = beta == 0.f ? alpha * s : beta * (*f) + alpha * s;
-    *f = val;
-    tileT[r * LDP + c] = val;
+  const int tid = threadIdx.x, r = tid >> 4, c4 = (tid & 15) * 4;
+  const float4* slab =
+      reinterpret_cast<const float4*>(J.slab + (size_t)tile * J.splits * TILE * TILE) +
+      (((s0 + r) * TILE + c4) >> 2);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int S = J.splits;
+  int sp = 0;
+  for (; sp + 4 <= S; sp += 4) {
+    const float4 a = slab[(size_t)(sp + 0) * (TILE * TILE / 4)];
+    const float4 b = slab[(size_t)(sp + 1) * (TILE * TILE / 4)];
+    const float4 c = slab[(size_t)(sp + 2) * (TILE * TILE / 4)];
+    const float4 d = slab[(size_t)(sp + 3) * (TILE * TILE / 4)];
+    acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+    acc.x += b.x; acc.y += b.y; acc.z += b.z; acc.w += b.w;
+    acc.x += c.x; acc.y += c.y; acc.z += c.z; acc.w += c.w;
+    acc.x += d.x; acc.y += d.y; acc.z += d.z; acc.w += d.w;
   }
-  if (diag) {  // mirror inside the diagonal tile
-    __syncthreads();
-    for (int e = threadIdx.x; e < TILE * TILE; e += NTHREADS) {
-      const int r = e >> 6, c = e & 63;  // write (r, c) for c > r from (c, r)
-      const int gi = i0 + r, gj = j0 + c;
-      if (c > r && gi < J.n && gj < J.n) J.F[(int64_t)gi * J.ldF + gj] = tileT[c * LDP + r];
-    }
-    return;
+  for (; sp < S; ++sp) {
+    const float4 a = slab[(size_t)sp * (TILE * TILE / 4)];
+    acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+  }
+  const float sum[4] = {acc.x, acc.y, acc.z, acc.w};
+  const int gi = i0 + s0 + r;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = c4 + q, gj = j0 + c;
+    if (gi >= n || gj >= n || (diag && c > s0 + r)) continue;
+    float* f = J.F + (int64_t)gi * J.ldF + gj;
+    const float val = J.beta == 0.f ? J.alpha * sum[q] : J.beta * (*f) + J.alpha * sum[q];
+    *f = val;
+    strip[r * LDP + c] = val;
   }
   __syncthreads();
-  // mirrored tile (j0.., i0..), coalesced along its rows
-  for (int e = threadIdx.x; e < TILE * TILE; e += NTHREADS) {
-    const int r = e >> 6, c = e & 63;
-    const int gi = j0 + r, gj = i0 + c;
-    if (gi < J.n && gj < J.n) J.F[(int64_t)gi * J.ldF + gj] = tileT[c * LDP + r];
+  // mirror: F[j0 + c][i0 + s0 + rr] = strip[rr][c] (diag tiles: strictly-lower sources only)
+  const int c = tid >> 2, r4 = (tid & 3) * 4;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int rr = r4 + q;
+    const int si = i0 + s0 + rr, sj = j0 + c;  // source element
+    if (si >= n || sj >= n || (diag && c >= s0 + rr)) continue;
+    J.F[(int64_t)sj * J.ldF + si] = strip[rr * LDP + c];
   }
 }
 
@@ -197,7 +212,7 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
   KFAC_CHECK_LAUNCH();
   {
     ProfScope ps(KFAC_PROF_FACTOR_REDUCE, stream);
-    hipLaunchKernelGGL(kfac_factor_reduce, dim3(tiles), dim3(NTHREADS), 0, stream, args);
+    hipLaunchKernelGGL(kfac_factor_reduce, dim3(tiles * 4), dim3(NTHREADS), 0, stream, args);
   }
   KFAC_CHECK_LAUNCH();
   return KFAC_OK;

@@ -5,17 +5,25 @@
 // without forming R^{-1}.  With P the exchange (flip) matrix:
 //   C = chol(P R P) (lower),  X = C^{-1} (lower),  L = P X^T P
 // satisfies L L^T = R^{-1}, L lower with a positive diagonal (= the unique
-// Cholesky factor of R^{-1}).  One potrf + one trtri instead of getrf/getri +
-// potrf; all arithmetic in fp64 (cond(R) reaches ~1e5 on the MLP).
+// Cholesky factor of R^{-1}).  One potrf whose elimination also yields the
+// inverse, instead of getrf/getri + potrf; all arithmetic in fp64 (cond(R)
+// reaches ~1e5 on the MLP).
 //
-// Blocked over 64x64 fp64 tiles, every launch grouped over ALL factors:
-//   inv_build            R' = P R P (damped, symmetrised, identity padded)
-//   for k: inv_panel(k)  factor the diagonal tile in LDS (LDL^T sweep that also
-//                        yields its inverse X[k][k]), then L[i][k] = W[i][k] X[k][k]^T
-//          inv_update(k) W[i][j] -= L[i][k] L[j][k]^T   (trailing lower tiles)
-//   for s = 1,2,4..: inv_trtri1/2 recursive doubling X21 = -X22 (C21 X11)
-//   [inv_xtx]            Y = X^T X (only for the full-inverse output)
-//   inv_out              L[i][j] = X[n-1-j][n-1-i]  (or R^{-1} = P Y P), fp32
+// Blocked over 64x64 fp64 tiles; every launch is grouped over ALL factors:
+//   inv_build       R' = P R P (damped, symmetrised, identity padded); Z = 0
+//   inv_update(-1)  factor tile (0,0): X[0][0] = chol(R'[0][0])^{-1}
+//   for k = 0..T-1:
+//     inv_panel(k)  C[i][k] = R'[i][k] X[k][k]^T          (i > k)
+//                   X[k][j] = X[k][k] Z[k][j]              (j < k)
+//     inv_update(k) R'[i][j] -= C[i][k] C[j][k]^T          (i >= j > k)
+//                   Z[i][j]  -= C[i][k] X[k][j]            (i > k >= j)
+//                   and the block owning (k+1,k+1) factors it right after its
+//                   update -> X[k+1][k+1] (one factorisation per step).
+//   [inv_xtx]       Y = X^T X (only for the full-inverse output)
+//   inv_out         L[i][j] = X[n-1-j][n-1-i]  (or R^{-1} = P Y P), fp32
+// Z (the partially eliminated identity) lives in X's lower tiles.  Tile GEMMs
+// use v_mfma_f64_16x16x4_f64; the 64x64 diagonal factorisation is blocked by 16
+// (one wave eliminates each 16x16 diagonal block, MFMA for the rest).
 #include <math.h>
 
 #include <algorithm>
@@ -24,28 +32,28 @@
 
 namespace kfac {
 
-constexpr int NB = 64;       // fp64 tile edge
-constexpr int DP = NB + 1;   // padded pitch (doubles)
+constexpr int NB = 64;      // fp64 tile edge
+constexpr int DP = NB + 2;  // LDS pitch (doubles): conflict-free MFMA operand reads
 constexpr int IMAXJ = 8;
+
+typedef double doublex4 __attribute__((ext_vector_type(4)));
 
 struct InvJobDev {
   const float* F;
   int64_t ldF;
   float* out;
   int64_t ldo;
-  double* W;   // Np x Np: R', then the Cholesky factor C (lower tiles)
-  double* X;   // Np x Np: C^{-1} (lower tiles)
-  double* Tm;  // Np x Np: scratch
+  double* W;   // Np x Np: R', then C below the diagonal (lower tiles)
+  double* X;   // Np x Np: Z accumulators, then C^{-1} (lower tiles)
+  double* Tm;  // Np x Np: scratch (X^T X)
   int* info;
   double scale, shift;
   int n, T, Np, kind;
-  // per-launch task geometry (filled by the host for the current launch)
-  int pairs_full, last_bottom;
 };
 
 struct InvArgs {
   int njobs;
-  int step;  // k for panel/update, s (tiles per half) for trtri
+  int step;
   int begin[IMAXJ + 1];
   InvJobDev job[IMAXJ];
 };
@@ -60,11 +68,16 @@ __device__ __forceinline__ double* tile_ptr(double* base, int Np, int ti, int tj
   return base + ((int64_t)ti * NB) * Np + (int64_t)tj * NB;
 }
 
+// All 16 loads of a thread are issued before the first LDS write (a rolled loop
+// would serialise 16 global-memory round trips).
 __device__ __forceinline__ void load_tile(double* lds, const double* g, int Np) {
-  for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
-    const int r = e >> 6, c = e & 63;
-    lds[r * DP + c] = g[(int64_t)r * Np + c];
-  }
+  constexpr int PER = NB * NB / NTHREADS;
+  const int c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+  double v[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) v[q] = g[(int64_t)(r0 + 4 * q) * Np + c];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) lds[(r0 + 4 * q) * DP + c] = v[q];
 }
 
 __device__ __forceinline__ void store_tile(double* g, const double* lds, int Np) {
@@ -74,225 +87,340 @@ __device__ __forceinline__ void store_tile(double* g, const double* lds, int Np)
   }
 }
 
+// ---------------------------------------------------------------- MFMA f64 blocks
+// One wave accumulates a 16x16 block: acc += A(16xK) * op(B), A rows at `a` (pitch
+// lda), B either (K x 16) at `b` (trans=false) or (16 x K) at `b` read as B^T.
+// v_mfma_f64_16x16x4_f64: lane l holds A[l&15][k0 + (l>>4)], B[k0 + (l>>4)][l&15];
+// result register v of lane l is C[(l>>4) + 4v][l&15].
+template <bool TRANS_B>
+__device__ __forceinline__ void mfma_block(const double* a, int lda, const double* b, int ldb, int K,
+                                           doublex4& acc) {
+  const int lane = threadIdx.x & 63;
+  const int i = lane & 15, kk = lane >> 4;
+  for (int k0 = 0; k0 < K; k0 += 4) {
+    const double av = a[i * lda + k0 + kk];
+    const double bv = TRANS_B ? b[i * ldb + k0 + kk] : b[(k0 + kk) * ldb + i];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ int acc_row64(int v) { return ((threadIdx.x & 63) >> 4) + 4 * v; }
+
+// Full 64x64 tile product into registers: wave w owns block row w, acc[jb] = block (w, jb).
+template <bool TRANS_B>
+__device__ __forceinline__ void gemm64(const double* A, const double* B, doublex4 (&acc)[4]) {
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb) {
+    acc[jb] = doublex4{0.0, 0.0, 0.0, 0.0};
+    if (TRANS_B)
+      mfma_block<true>(A + 16 * w * DP, DP, B + 16 * jb * DP, DP, NB, acc[jb]);
+    else
+      mfma_block<false>(A + 16 * w * DP, DP, B + 16 * jb, DP, NB, acc[jb]);
+  }
+}
+
+// global[tile](r, c) = alpha * acc (+ global if accumulate)   (acc from gemm64)
+__device__ __forceinline__ void store_acc_global(double* g, int Np, const doublex4 (&acc)[4],
+                                                 double alpha, bool accumulate) {
+  const int w = threadIdx.x >> 6, col = threadIdx.x & 15;
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      double* p = g + (int64_t)(16 * w + acc_row64(v)) * Np + 16 * jb + col;
+      *p = accumulate ? *p + alpha * acc[jb][v] : alpha * acc[jb][v];
+    }
+}
+
+// 1/d: v_rcp_f64 + two Newton steps (~1 ulp) instead of the IEEE division sequence,
+// which sits on the elimination's serial chain.
+__device__ __forceinline__ double fast_rcp(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+
+// --------------------------------------------------------- diagonal factorisation
+// S (64x64 lower, LDS) -> Y = chol(S)^{-1} (lower, LDS); S is destroyed.
+// Blocked by 16: wave 0 eliminates each 16x16 diagonal block [D | I] -> I_k =
+// D^{-1/2} L_unit^{-1}; the panel (C = S I_k^T, X_k = I_k Z_k) and the trailing /
+// Z updates are 16x16 MFMA blocks spread over the 4 waves.  dg (>= NB+352 doubles)
+// receives the pivots; its tail is scratch.
+template <int PARTS = 7>  // ablation: bit0 elimination, bit1 panel, bit2 trailing
+__device__ void diag_factor(double* S, double* Y, double* dg) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int e = tid; e < NB * NB; e += NTHREADS) Y[(e >> 6) * DP + (e & 63)] = 0.0;
+  __syncthreads();
+  for (int kb = 0; kb < 4; ++kb) {
+    const int o = 16 * kb;
+    // (1) one wave: unit-lower elimination of the 16x16 diagonal block [D | I] -> I_k.
+    // Lane (r, g) keeps D[r][4g..4g+3] and Y[r][4g..4g+3] in registers; per column
+    // the owners publish column j of D and row j of Y to LDS (`bc`, `by`), and every
+    // lane reads what it needs in one batch (LDS ops of one wave complete in order,
+    // so no barrier), then updates with selects (no divergent branches).
+    if ((PARTS & 1) && wave == 0) {
+      double* Sb = S + o * DP + o;
+      double* Yb = Y + o * DP + o;
+      double* bc = dg + NB;       // column j of D: 16 slots + 64 dummy slots
+      double* by = dg + NB + 80;  // row j of Y: 16 slots + 4*64 dummy slots
+      const int r = lane & 15, g = lane >> 4;
+      double sv[4], yv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        sv[q] = Sb[r * DP + 4 * g + q];
+        yv[q] = (r == 4 * g + q) ? 1.0 : 0.0;
+      }
+      double piv = 1.0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        // every lane writes (non-owners into private dummy slots): no divergent branches
+        bc[(g == (j >> 2)) ? r : 16 + lane] = sv[j & 3];
+        double* yw = by + ((r == j) ? 4 * g : 16 + 4 * lane);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) yw[q] = yv[q];
+        const double d = bc[j];
+        const double srj = bc[r];
+        double sc[4], yj[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          sc[q] = bc[4 * g + q];
+          yj[q] = by[4 * g + q];
+        }
+        piv = (r == j) ? d : piv;
+        const double l = srj / d;
+        const bool below = r > j;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = 4 * g + q;
+          const double ns = sv[q] - l * sc[q];
+          const double ny = yv[q] - l * yj[q];
+          sv[q] = (below && c > j) ? ns : sv[q];
+          yv[q] = (below && c <= j) ? ny : yv[q];
+        }
+      }
+      if (g == 0) dg[o + r] = piv;
+      const double rs = 1.0 / sqrt(piv);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Yb[r * DP + 4 * g + q] = (4 * g + q <= r) ? yv[q] * rs : 0.0;
+    }
+    __syncthreads();
+    // (2) panel: blocks ib > kb: C = S[ib][kb] I^T ;  blocks jb < kb: X = I Z[kb][jb]
+    const int nC = 3 - kb, nX = kb;
+    doublex4 acc = {0.0, 0.0, 0.0, 0.0};
+    int mine = -1;
+    if ((PARTS & 2) && wave < nC + nX) {  // nC + nX = 3: at most one block per wave
+      mine = wave;
+      if (wave < nC) {
+        const int ib = kb + 1 + wave;
+        mfma_block<true>(S + 16 * ib * DP + o, DP, Y + o * DP + o, DP, 16, acc);
+      } else {
+        const int jb = wave - nC;
+        mfma_block<false>(Y + o * DP + o, DP, Y + o * DP + 16 * jb, DP, 16, acc);
+      }
+    }
+    __syncthreads();
+    if (mine >= 0) {
+      const int col = lane & 15;
+      double* dst = (mine < nC) ? S + 16 * (kb + 1 + mine) * DP + o : Y + o * DP + 16 * (mine - nC);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) dst[acc_row64(v) * DP + col] = acc[v];
+    }
+    __syncthreads();
+    if (kb == 3) break;
+    // (3) trailing: S[ib][jb] -= C[ib] C[jb]^T (kb < jb <= ib); Z[ib][jb] -= C[ib] X[kb][jb] (jb <= kb)
+    const int nT = (3 - kb) * (4 - kb) / 2, nZ = (3 - kb) * (kb + 1);
+    for (int t = wave; (PARTS & 4) && t < nT + nZ; t += 4) {
+      doublex4 a2 = {0.0, 0.0, 0.0, 0.0};
+      double* dst;
+      if (t < nT) {
+        int i = 0;
+        while ((i + 1) * (i + 2) / 2 <= t) ++i;
+        const int ib = kb + 1 + i, jb = kb + 1 + (t - i * (i + 1) / 2);
+        mfma_block<true>(S + 16 * ib * DP + o, DP, S + 16 * jb * DP + o, DP, 16, a2);
+        dst = S + 16 * ib * DP + 16 * jb;
+      } else {
+        const int u = t - nT;
+        const int ib = kb + 1 + u / (kb + 1), jb = u % (kb + 1);
+        mfma_block<false>(S + 16 * ib * DP + o, DP, Y + o * DP + 16 * jb, DP, 16, a2);
+        dst = Y + 16 * ib * DP + 16 * jb;
+      }
+      const int col = lane & 15;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) dst[acc_row64(v) * DP + col] -= a2[v];
+    }
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------------- build R'
+// R'[i][c] = scale*(F[fi][fc] + F[fc][fi])/2 + shift*[i==c], fi = n-1-i, fc = n-1-c.
+// Both source blocks are read row-coalesced into LDS (fp32), then combined.
 __global__ __launch_bounds__(NTHREADS) void inv_build(InvArgs args) {
+  __shared__ float P[NB * (NB + 1)];  // P[a][b] = F[fi(a)][fc(b)]
+  __shared__ float Q[NB * (NB + 1)];  // Q[b][a] = F[fc(b)][fi(a)]
   const int j = find_job(args, blockIdx.x);
   const InvJobDev& J = args.job[j];
   int ti, tj;
   tri_decode(blockIdx.x - args.begin[j], ti, tj);
-  const int n = J.n;
-  for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
-    const int i = ti * NB + (e >> 6), c = tj * NB + (e & 63);
+  const int n = J.n, i0 = ti * NB, c0 = tj * NB;
+  constexpr int PER = NB * NB / NTHREADS;
+  const int cc = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+  float pv[PER], qv[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int a = r0 + 4 * q;
+    // row fi = n-1-(i0+a), column fc = n-1-(c0+cc): consecutive lanes -> consecutive fc (descending)
+    const int i = i0 + a, c = c0 + cc;
+    pv[q] = (i < n && c < n) ? J.F[(int64_t)(n - 1 - i) * J.ldF + (n - 1 - c)] : 0.f;
+    const int ib = i0 + cc, cb = c0 + a;  // Q[a][cc] = F[n-1-(c0+a)][n-1-(i0+cc)]
+    qv[q] = (ib < n && cb < n) ? J.F[(int64_t)(n - 1 - cb) * J.ldF + (n - 1 - ib)] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    P[(r0 + 4 * q) * (NB + 1) + cc] = pv[q];
+    Q[(r0 + 4 * q) * (NB + 1) + cc] = qv[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int a = r0 + 4 * q, i = i0 + a, c = c0 + cc;
     double v;
     if (i < n && c < n) {
-      const int fi = n - 1 - i, fc = n - 1 - c;  // flip
-      const double sym = 0.5 * ((double)J.F[(int64_t)fi * J.ldF + fc] +
-                                (double)J.F[(int64_t)fc * J.ldF + fi]);
+      const double sym = 0.5 * ((double)P[a * (NB + 1) + cc] + (double)Q[cc * (NB + 1) + a]);
       v = J.scale * sym + (i == c ? J.shift : 0.0);
     } else {
       v = (i == c) ? 1.0 : 0.0;  // identity padding keeps the padded block trivial
     }
     J.W[(int64_t)i * J.Np + c] = v;
+    if (ti != tj) J.X[(int64_t)i * J.Np + c] = 0.0;  // Z accumulators start at 0
   }
 }
 
-// -------------------------------------------------------------- panel step k
-// Every block of the panel factors the (k,k) tile in LDS (cheap, avoids a launch):
-// LDL^T sweep with the unit-lower inverse carried along (Gaussian elimination on
-// [S | I] gives [D L^T | L_unit^{-1}]), then
-//   Lkk = L_unit D^{1/2},  Xkk = D^{-1/2} L_unit^{-1}.
-__global__ __launch_bounds__(NTHREADS) void inv_panel(InvArgs args) {
-  __shared__ double S[NB * DP];
-  __shared__ double Y[NB * DP];
-  __shared__ double P[NB * DP];
-  __shared__ double dg[NB];
+// ------------------------------------------------------------------- update k
+__global__ __launch_bounds__(NTHREADS) void inv_update(InvArgs args) {
+  __shared__ __attribute__((aligned(16))) double A[NB * DP];
+  __shared__ __attribute__((aligned(16))) double B[NB * DP];
+  __shared__ __attribute__((aligned(16))) double Y[NB * DP];
+  __shared__ double dg[NB + 352];  // pivots + elimination broadcast buffers
   const int jb = find_job(args, blockIdx.x);
   const InvJobDev& J = args.job[jb];
-  const int k = args.step;
-  const int i = k + (blockIdx.x - args.begin[jb]);
-  const int tid = threadIdx.x;
-
-  load_tile(S, tile_ptr(J.W, J.Np, k, k), J.Np);
-  for (int e = tid; e < NB * NB; e += NTHREADS) Y[(e >> 6) * DP + (e & 63)] = ((e >> 6) == (e & 63)) ? 1.0 : 0.0;
-  if (i != k) load_tile(P, tile_ptr(J.W, J.Np, i, k), J.Np);
-  __syncthreads();
-
-  const int cc = tid & 63, r0 = tid >> 6;
-  for (int jj = 0; jj < NB; ++jj) {
-    const double d = S[jj * DP + jj];
-    if (tid == 0) dg[jj] = d;
-    const double inv = 1.0 / d;
-    for (int r = jj + 1 + r0; r < NB; r += 4) {
-      if (cc > r) continue;
-      const double l = S[r * DP + jj] * inv;
-      if (cc <= jj)
-        Y[r * DP + cc] -= l * Y[jj * DP + cc];
-      else
-        S[r * DP + cc] -= l * S[cc * DP + jj];
+  const int k = args.step, T = J.T;
+  const int local = blockIdx.x - args.begin[jb];
+  const int nTrail = (T - k - 1) * (T - k) / 2;
+  if (k < 0 || local < nTrail) {
+    int i = k + 1, j = k + 1;
+    if (k >= 0) {
+      int a, b;
+      tri_decode(local, a, b);
+      i = k + 1 + a;
+      j = k + 1 + b;
     }
+    const bool factor = (i == k + 1 && j == k + 1);
+    doublex4 acc[4];
+    if (k >= 0) {
+      load_tile(A, tile_ptr(J.W, J.Np, i, k), J.Np);
+      load_tile(B, tile_ptr(J.W, J.Np, j, k), J.Np);
+      __syncthreads();
+      gemm64<true>(A, B, acc);
+    }
+    if (!factor) {
+      store_acc_global(tile_ptr(J.W, J.Np, i, j), J.Np, acc, -1.0, true);
+      return;
+    }
+    // the updated diagonal tile is consumed right here (never written back)
     __syncthreads();
-  }
-  // Xkk = D^{-1/2} L_unit^{-1} (zero upper).  The factored diagonal tile itself is
-  // never needed again (the panel and the inverse only use Xkk), so W[k][k] is
-  // left as is: the other blocks of this launch may still be reading it.
-  for (int e = tid; e < NB * NB; e += NTHREADS) {
-    const int r = e >> 6, c = e & 63;
-    const double xv = (r > c) ? Y[r * DP + c] / sqrt(dg[r]) : (r == c ? 1.0 / sqrt(dg[r]) : 0.0);
-    Y[r * DP + c] = xv;
-  }
-  __syncthreads();
-  if (i == k) {
-    if (tid == 0 && J.info) {
+    load_tile(A, tile_ptr(J.W, J.Np, i, i), J.Np);
+    __syncthreads();
+    if (k >= 0) {
+      const int w = threadIdx.x >> 6, col = threadIdx.x & 15;
+#pragma unroll
+      for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) A[(16 * w + acc_row64(v)) * DP + 16 * b4 + col] -= acc[b4][v];
+      __syncthreads();
+    }
+    diag_factor(A, Y, dg);
+    if (threadIdx.x == 0 && J.info) {
       for (int c = 0; c < NB; ++c) {
-        const int g = k * NB + c;
+        const int g = i * NB + c;
         if (g < J.n && !(dg[c] > 0.0)) {
           atomicCAS(J.info, 0, g + 1);
           break;
         }
       }
     }
-    store_tile(tile_ptr(J.X, J.Np, k, k), Y, J.Np);
+    store_tile(tile_ptr(J.X, J.Np, i, i), Y, J.Np);
     return;
   }
-  // L[i][k] = W[i][k] * Xkk^T  (64x64x64 fp64, 4x4 outputs per thread)
-  const int tr = tid >> 4, tc = tid & 15;
-  double acc[4][4] = {};
-  for (int m = 0; m < NB; ++m) {
-    double a[4], b[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) a[q] = P[(tr * 4 + q) * DP + m];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) b[p] = Y[(tc * 4 + p) * DP + m];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int p = 0; p < 4; ++p) acc[q][p] += a[q] * b[p];
-  }
-  double* dst = tile_ptr(J.W, J.Np, i, k);
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int p = 0; p < 4; ++p) dst[(int64_t)(tr * 4 + q) * J.Np + tc * 4 + p] = acc[q][p];
-}
-
-// ------------------------------------------------------------- update step k
-__global__ __launch_bounds__(NTHREADS) void inv_update(InvArgs args) {
-  __shared__ double A[NB * DP];
-  __shared__ double B[NB * DP];
-  const int jb = find_job(args, blockIdx.x);
-  const InvJobDev& J = args.job[jb];
-  const int k = args.step;
-  int a, b;
-  tri_decode(blockIdx.x - args.begin[jb], a, b);
-  const int i = k + 1 + a, jj = k + 1 + b;
+  // Z[i][j] -= C[i][k] X[k][j]   (i > k >= j)
+  const int u = local - nTrail;
+  const int i = k + 1 + u / (k + 1), j = u % (k + 1);
   load_tile(A, tile_ptr(J.W, J.Np, i, k), J.Np);
-  load_tile(B, tile_ptr(J.W, J.Np, jj, k), J.Np);
+  load_tile(B, tile_ptr(J.X, J.Np, k, j), J.Np);
   __syncthreads();
-  const int tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
-  double acc[4][4] = {};
-  for (int m = 0; m < NB; ++m) {
-    double x[4], y[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) x[q] = A[(tr * 4 + q) * DP + m];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) y[p] = B[(tc * 4 + p) * DP + m];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int p = 0; p < 4; ++p) acc[q][p] += x[q] * y[p];
-  }
-  double* dst = tile_ptr(J.W, J.Np, i, jj);
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int p = 0; p < 4; ++p) dst[(int64_t)(tr * 4 + q) * J.Np + tc * 4 + p] -= acc[q][p];
+  doublex4 acc[4];
+  gemm64<false>(A, B, acc);
+  store_acc_global(tile_ptr(J.X, J.Np, i, j), J.Np, acc, -1.0, true);
 }
 
-// ------------------------------------------- tile GEMM: C = alpha * sum_m A(.,m) B(m,.)
-// transA: A tile (r, m) read as Abase tile (m, r) transposed.
-__device__ void tile_gemm_sum(const double* Abase, const double* Bbase, int Np, int ar, int bc,
-                              int m0, int m1, bool transA, double alpha, double* C, double* sA,
-                              double* sB) {
-  const int tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
-  double acc[4][4] = {};
-  for (int m = m0; m < m1; ++m) {
-    if (transA)
-      load_tile(sA, Abase + ((int64_t)m * NB) * Np + (int64_t)ar * NB, Np);
-    else
-      load_tile(sA, Abase + ((int64_t)ar * NB) * Np + (int64_t)m * NB, Np);
-    load_tile(sB, Bbase + ((int64_t)m * NB) * Np + (int64_t)bc * NB, Np);
-    __syncthreads();
-    for (int mm = 0; mm < NB; ++mm) {
-      double x[4], y[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        x[q] = transA ? sA[mm * DP + tr * 4 + q] : sA[(tr * 4 + q) * DP + mm];
-#pragma unroll
-      for (int p = 0; p < 4; ++p) y[p] = sB[mm * DP + tc * 4 + p];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int p = 0; p < 4; ++p) acc[q][p] += x[q] * y[p];
-    }
-    __syncthreads();
-  }
-  double* dst = C + ((int64_t)ar * NB) * Np + (int64_t)bc * NB;
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int p = 0; p < 4; ++p) dst[(int64_t)(tr * 4 + q) * Np + tc * 4 + p] = alpha * acc[q][p];
-}
-
-// task -> (t0, bottom tile bi, top tile aj) for pair geometry at half-size s
-__device__ __forceinline__ void pair_decode(const InvJobDev& J, int s, int local, int& t0, int& bi,
-                                            int& aj) {
-  const int full = J.pairs_full * s * s;
-  int p, rem;
-  if (local < full) {
-    p = local / (s * s);
-    rem = local - p * s * s;
-  } else {
-    p = J.pairs_full;
-    rem = local - full;
-  }
-  t0 = p * 2 * s;
-  bi = t0 + s + rem / s;
-  aj = t0 + rem % s;
-}
-
-// T1[bi][aj] = sum_{m in top, m >= aj} C[bi][m] X[m][aj]
-__global__ __launch_bounds__(NTHREADS) void inv_trtri1(InvArgs args) {
-  __shared__ double sA[NB * DP];
-  __shared__ double sB[NB * DP];
+// -------------------------------------------------------------------- panel k
+__global__ __launch_bounds__(NTHREADS) void inv_panel(InvArgs args) {
+  __shared__ __attribute__((aligned(16))) double A[NB * DP];
+  __shared__ __attribute__((aligned(16))) double Xk[NB * DP];
   const int jb = find_job(args, blockIdx.x);
   const InvJobDev& J = args.job[jb];
-  const int s = args.step;
-  int t0, bi, aj;
-  pair_decode(J, s, blockIdx.x - args.begin[jb], t0, bi, aj);
-  tile_gemm_sum(J.W, J.X, J.Np, bi, aj, aj, t0 + s, false, 1.0, J.Tm, sA, sB);
-}
-
-// X[bi][aj] = - sum_{m in bottom, m <= bi} X[bi][m] T1[m][aj]
-__global__ __launch_bounds__(NTHREADS) void inv_trtri2(InvArgs args) {
-  __shared__ double sA[NB * DP];
-  __shared__ double sB[NB * DP];
-  const int jb = find_job(args, blockIdx.x);
-  const InvJobDev& J = args.job[jb];
-  const int s = args.step;
-  int t0, bi, aj;
-  pair_decode(J, s, blockIdx.x - args.begin[jb], t0, bi, aj);
-  tile_gemm_sum(J.X, J.Tm, J.Np, bi, aj, t0 + s, bi + 1, false, -1.0, J.X, sA, sB);
+  const int k = args.step, T = J.T;
+  const int local = blockIdx.x - args.begin[jb];
+  const int nC = T - k - 1;
+  load_tile(Xk, tile_ptr(J.X, J.Np, k, k), J.Np);
+  doublex4 acc[4];
+  if (local < nC) {  // C[i][k] = R'[i][k] X[k][k]^T
+    const int i = k + 1 + local;
+    double* t = tile_ptr(J.W, J.Np, i, k);
+    load_tile(A, t, J.Np);
+    __syncthreads();
+    gemm64<true>(A, Xk, acc);
+    store_acc_global(t, J.Np, acc, 1.0, false);
+  } else {           // X[k][j] = X[k][k] Z[k][j]
+    const int j = local - nC;
+    double* t = tile_ptr(J.X, J.Np, k, j);
+    load_tile(A, t, J.Np);
+    __syncthreads();
+    gemm64<false>(Xk, A, acc);
+    store_acc_global(t, J.Np, acc, 1.0, false);
+  }
 }
 
 // Y[a][b] = sum_{m >= a} X[m][a]^T X[m][b]   (lower tiles, a >= b)
 __global__ __launch_bounds__(NTHREADS) void inv_xtx(InvArgs args) {
-  __shared__ double sA[NB * DP];
-  __shared__ double sB[NB * DP];
+  __shared__ __attribute__((aligned(16))) double A[NB * DP];
+  __shared__ __attribute__((aligned(16))) double B[NB * DP];
   const int jb = find_job(args, blockIdx.x);
   const InvJobDev& J = args.job[jb];
   int a, b;
   tri_decode(blockIdx.x - args.begin[jb], a, b);
-  tile_gemm_sum(J.X, J.X, J.Np, a, b, a, J.T, true, 1.0, J.Tm, sA, sB);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  doublex4 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = doublex4{0.0, 0.0, 0.0, 0.0};
+  for (int m = a; m < J.T; ++m) {
+    load_tile(A, tile_ptr(J.X, J.Np, m, a), J.Np);  // read transposed below
+    load_tile(B, tile_ptr(J.X, J.Np, m, b), J.Np);
+    __syncthreads();
+    const int i = lane & 15, kk = lane >> 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      for (int k0 = 0; k0 < NB; k0 += 4) {
+        const double av = A[(k0 + kk) * DP + 16 * w + i];  // (X^T)[row][k] = X[k][row]
+        const double bv = B[(k0 + kk) * DP + 16 * q + i];
+        acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[q], 0, 0, 0);
+      }
+    __syncthreads();
+  }
+  store_acc_global(tile_ptr(J.Tm, J.Np, a, b), J.Np, acc, 1.0, false);
 }
 
 // ------------------------------------------------------------------- output
@@ -370,26 +498,16 @@ static int invert_group(const kfac_invert_job* jobs, int njobs, char* ws, int32_
   }
   rc = launch(inv_build, args, [](const InvJobDev& d) { return d.T * (d.T + 1) / 2; }, s);
   if (rc) return rc;
+  args.step = -1;
+  rc = launch(inv_update, args, [](const InvJobDev&) { return 1; }, s);
+  if (rc) return rc;
   for (int k = 0; k < Tmax; ++k) {
     args.step = k;
-    rc = launch(inv_panel, args, [k](const InvJobDev& d) { return k < d.T ? d.T - k : 0; }, s);
+    rc = launch(inv_panel, args, [k](const InvJobDev& d) { return k < d.T ? d.T - 1 : 0; }, s);
     if (rc) return rc;
-    rc = launch(inv_update, args,
-                [k](const InvJobDev& d) { return k < d.T ? (d.T - k - 1) * (d.T - k) / 2 : 0; }, s);
-    if (rc) return rc;
-  }
-  for (int sz = 1; sz < Tmax; sz *= 2) {
-    args.step = sz;
-    for (int j = 0; j < njobs; ++j) {
-      InvJobDev& d = args.job[j];
-      d.pairs_full = d.T / (2 * sz);
-      const int rest = d.T - d.pairs_full * 2 * sz;
-      d.last_bottom = std::max(0, rest - sz);
-    }
-    auto count = [sz](const InvJobDev& d) { return d.pairs_full * sz * sz + d.last_bottom * sz; };
-    rc = launch(inv_trtri1, args, count, s);
-    if (rc) return rc;
-    rc = launch(inv_trtri2, args, count, s);
+    rc = launch(inv_update, args, [k](const InvJobDev& d) {
+      return k + 1 < d.T ? (d.T - k - 1) * (d.T - k) / 2 + (d.T - k - 1) * (k + 1) : 0;
+    }, s);
     if (rc) return rc;
   }
   if (any_inverse) {

@@ -17,7 +17,7 @@ constexpr int TILE = 64;        // output tile edge
 constexpr int BK = 32;          // rows of k staged per pipeline step
 constexpr int LDP = TILE + 1;   // padded LDS row pitch (floats): column writes conflict-free
 constexpr int NTHREADS = 256;   // 4 waves
-constexpr int PANEL = BK * LDP; // floats per staged panel
+constexpr int PANEL = BK * (TILE + 4); // floats per staged panel (max pitch)
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
@@ -70,34 +70,54 @@ static inline OpDev to_dev(const kfac_operand& o) {
 template <int LAYOUT>
 struct Panel;
 
+// ROWMAJOR: 16-byte loads (16 lanes cover one 256-byte panel row) and
+// ds_write_b128 into a [k][i] image with a 16-byte-aligned pitch; columns at the
+// right edge (ones column, ragged widths, unaligned rows) fall back to scalars.
 template <>
 struct Panel<KFAC_ROWMAJOR> {
+  static constexpr int PITCH = TILE + 4;
   const float* base;
   int64_t ld, kend;
-  int col, c, r0, cols, ones;
+  int col, c4, r0, cols, ones;
+  bool vec;
   __device__ __forceinline__ void init(const OpDev& op, int col0, int tid, int64_t k_end) {
     base = op.ptr; ld = op.ld; kend = k_end; cols = op.cols; ones = op.ones;
-    c = tid & 63; r0 = tid >> 6; col = col0 + c;
+    c4 = (tid & 15) * 4; r0 = tid >> 4; col = col0 + c4;
+    vec = (col + 3 < cols) && ((ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(base) & 15) == 0);
   }
   __device__ __forceinline__ void load(int64_t k, float (&v)[8]) const {
-    const bool real = col < cols;
-    const float fill = (col == ones) ? 1.f : 0.f;
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      const int64_t row = k + r0 + 4 * m;
-      float x = 0.f;
-      if (row < kend) x = real ? base[row * ld + col] : fill;
-      v[m] = x;
+    for (int m = 0; m < 2; ++m) {
+      const int64_t row = k + r0 + 16 * m;
+      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row < kend) {
+        const float* p = base + row * ld + col;
+        if (vec) {
+          x = *reinterpret_cast<const float4*>(p);
+        } else {
+          float e[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int cq = col + q;
+            e[q] = cq < cols ? p[q] : (cq == ones ? 1.f : 0.f);
+          }
+          x = make_float4(e[0], e[1], e[2], e[3]);
+        }
+      }
+      v[4 * m + 0] = x.x; v[4 * m + 1] = x.y; v[4 * m + 2] = x.z; v[4 * m + 3] = x.w;
     }
   }
   __device__ __forceinline__ void store(float* lds, const float (&v)[8]) const {
 #pragma unroll
-    for (int m = 0; m < 8; ++m) lds[(r0 + 4 * m) * LDP + c] = v[m];
+    for (int m = 0; m < 2; ++m)
+      *reinterpret_cast<float4*>(lds + (r0 + 16 * m) * PITCH + c4) =
+          make_float4(v[4 * m], v[4 * m + 1], v[4 * m + 2], v[4 * m + 3]);
   }
 };
 
 template <>
 struct Panel<KFAC_CHANNEL> {
+  static constexpr int PITCH = LDP;
   const float* base;
   int64_t L, sB, kend;
   int r, c0, col0, cols, ones;
@@ -129,6 +149,7 @@ struct Panel<KFAC_CHANNEL> {
 
 template <>
 struct Panel<KFAC_PATCH> {
+  static constexpr int PITCH = LDP;
   static constexpr int KZERO = -1, KONES = -2;
   const float* base;
   int64_t L, sB, kend;
@@ -223,11 +244,12 @@ __device__ __forceinline__ void contract_tile(const OpDev& opA, int i0, const Op
     }
     float* bcur = lds + 2 * cur * PANEL;
     if (active) {
-      const float* a = bcur + h * LDP + qi * 32 + rr;
-      const float* b = bcur + (same ? 0 : PANEL) + h * LDP + qj * 32 + rr;
+      const float* a = bcur + h * Panel<LA>::PITCH + qi * 32 + rr;
+      const float* b = bcur + (same ? 0 : PANEL) + h * Panel<LB>::PITCH + qj * 32 + rr;
 #pragma unroll
       for (int s = 0; s < BK / 2; ++s)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[2 * s * LDP], b[2 * s * LDP], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[2 * s * Panel<LA>::PITCH],
+                                                   b[2 * s * Panel<LB>::PITCH], acc, 0, 0, 0);
     }
     if (more) {
       float* bnext = lds + 2 * (cur ^ 1) * PANEL;

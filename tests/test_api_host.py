@@ -1,0 +1,139 @@
+"""CPU: the drop-in's host-side contract (models/curvatures.py:38-65, 295-398 semantics)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+import host_double
+from oracle import kfac_oracle as O
+
+
+def mlp():
+    torch.manual_seed(0)
+    return nn.Sequential(nn.Linear(6, 5), nn.ReLU(), nn.Linear(5, 3))
+
+
+def test_layer_type_selection():
+    from bnn_kfac_amd.curvatures import KFAC
+    net = mlp()
+    assert KFAC(net, 'Linear').layer_types == ['Linear']
+    assert KFAC(net, []).layer_types == ['Linear', 'Conv2d', 'MultiheadAttention']
+    assert KFAC(net, None).layer_types == ['Linear', 'Conv2d', 'MultiheadAttention']
+    with pytest.raises(TypeError):
+        KFAC(net, 5)
+    with pytest.raises(AssertionError):
+        KFAC(net, ['Dense'])
+    k = KFAC(net, ['Conv2d'])
+    assert k.record == {} and k.hooks == []
+
+
+def test_multihead_attention_not_implemented():
+    from bnn_kfac_amd.curvatures import KFAC
+    net = nn.Sequential(nn.MultiheadAttention(8, 2))
+    with pytest.raises(NotImplementedError):
+        KFAC(net)
+    KFAC(net, 'Linear')  # excluding the type skips it (its out_proj is a Linear subclass)
+
+
+def test_hooks_record_input_and_scaled_grad_output():
+    from bnn_kfac_amd.curvatures import KFAC
+    net = mlp()
+    kfac = KFAC(net)
+    x = torch.rand(4, 6)
+    out = net(x)
+    out.sum().div(4).backward()
+    a, g = kfac.record[net[0]]
+    assert a is x  # reference keeps the input itself (curvatures.py:319-320)
+    # grad_output * batch (curvatures.py:322-323): d(sum/4)/d(out) * 4 = 1 for the last layer
+    assert torch.allclose(kfac.record[net[2]][1], torch.ones(4, 3))
+    assert g.shape == (4, 5)
+
+
+def test_invert_requires_state():
+    from bnn_kfac_amd.curvatures import KFAC
+    with pytest.raises(AssertionError, match="State dict is empty"):
+        KFAC(mlp()).invert(1.0, 1.0)
+
+
+def test_no_cpu_fallback():
+    from bnn_kfac_amd import _native as N
+    from bnn_kfac_amd.curvatures import KFAC
+    net = mlp()
+    kfac = KFAC(net)
+    net(torch.rand(3, 6)).sum().backward()
+    with pytest.raises(N.NativeError, match="no CPU fallback"):
+        kfac.update(3)
+
+
+def test_damping_argument_handling():
+    from bnn_kfac_amd.curvatures import KFAC
+    kfac = KFAC(mlp())
+    kfac.state = {1: None, 2: None}
+    assert kfac._damping(0.04, 200) == [(0.04, 200.0), (0.04, 200.0)]
+    assert kfac._damping([1, 2], [3, 4]) == [(1, 3), (2, 4)]
+    with pytest.raises(AssertionError):
+        kfac._damping([1], [3, 4])
+    with pytest.raises(TypeError):  # mixed list/scalar: float(list) (curvatures.py:378)
+        kfac._damping([1, 2], 3.0)
+
+
+def test_update_host_logic_with_double(monkeypatch):
+    """Packed buffer, per-batch alpha, first-assign / then-accumulate, modules() order."""
+    from bnn_kfac_amd.curvatures import KFAC
+    host_double.install(monkeypatch)
+    net = mlp()
+    kfac = KFAC(net)
+    ref = O.OracleKFAC(np.float64)
+    rng = np.random.default_rng(0)
+    for B in (7, 7, 3):
+        a1 = rng.random((B, 6), dtype=np.float32)
+        g1 = rng.standard_normal((B, 5)).astype(np.float32)
+        a2 = rng.random((B, 5), dtype=np.float32)
+        g2 = rng.standard_normal((B, 3)).astype(np.float32)
+        kfac.record[net[0]] = [torch.from_numpy(a1), torch.from_numpy(g1)]
+        kfac.record[net[2]] = [torch.from_numpy(a2), torch.from_numpy(g2)]
+        kfac.update(B)
+        ref.update_linear("l0", a1, g1, True)
+        ref.update_linear("l1", a2, g2, True)
+    assert list(kfac.state) == [net[0], net[2]]
+    A0, G0 = kfac.state[net[0]]
+    assert A0.data_ptr() == kfac._packed.data_ptr()  # first factor at the buffer start
+    np.testing.assert_allclose(A0.numpy(), ref.state["l0"][0], rtol=1e-5)
+    np.testing.assert_allclose(G0.numpy(), ref.state["l0"][1], rtol=1e-5)
+    np.testing.assert_allclose(kfac.state[net[2]][0].numpy(), ref.state["l1"][0], rtol=1e-5)
+    kfac.reset()
+    assert kfac.state == {} and kfac._packed is not None
+
+
+def test_save_load_roundtrip(tmp_path):
+    from bnn_kfac_amd.curvatures import KFAC
+    net = mlp()
+    kfac = KFAC(net)
+    kfac.state = {net[0]: [torch.eye(7), torch.eye(5)], net[2]: [torch.eye(6), torch.eye(3)]}
+    kfac.inv_state = {net[0]: (torch.eye(7) * 2, torch.eye(5) * 2)}
+    fn = str(tmp_path / "kfac.pt")
+    kfac.save(fn)
+    other = KFAC(mlp())
+    other.load(fn)
+    assert [type(m).__name__ for m in other.state] == ["Linear", "Linear"]
+    assert torch.equal(other.state[other.model[0]][0], torch.eye(7))
+    assert torch.equal(other.inv_state[other.model[0]][1], torch.eye(5) * 2)
+    for p, q in zip(net.parameters(), other.model.parameters()):
+        assert torch.equal(p, q)
+
+
+def test_kron_doctest():
+    import doctest
+
+    from bnn_kfac_amd import utilities
+    res = doctest.testmod(utilities)
+    assert res.failed == 0 and res.attempted >= 1
+
+
+def test_variance_helpers():
+    from bnn_kfac_amd.variance import argmax_grad_outputs, entropy_bits
+    p = torch.tensor([[0.1, 0.7, 0.2], [0.5, 0.2, 0.3]])
+    go = argmax_grad_outputs(p)
+    # classification_ll_block.py:119-121: every argmax column set in EVERY row
+    assert torch.equal(go, torch.tensor([[1., 1., 0.], [1., 1., 0.]]))
+    assert abs(entropy_bits(1.0) - 0.5 * np.log2(2 * np.e * np.pi)) < 1e-12
