@@ -26,6 +26,7 @@ struct FactorJobDev {
   int64_t chunk;     // rows per split (multiple of BK)
   int n, t, splits;  // factor edge, tiles per edge, K-splits
   int task_begin;    // first global task of this job
+  int glds;          // row-major, 16-byte-aligned rows: LDS-DMA kernel
   int tile_begin;    // first global tile of this job (reduce launch)
 };
 
@@ -38,7 +39,9 @@ struct FactorArgs {
 
 template <int LAYOUT>
 __device__ __forceinline__ void factor_task(const FactorJobDev& J, int local, float* lds) {
-  const int tile = local / J.splits, split = local - tile * J.splits;
+  // split-major order: consecutive tasks share the rows [k0, k1) of the operand
+  const int tiles = J.t * (J.t + 1) / 2;
+  const int split = local / tiles, tile = local - split * tiles;
   int ti, tj;
   tri_decode(tile, ti, tj);
   const int64_t k0 = (int64_t)split * J.chunk;
@@ -52,19 +55,169 @@ __device__ __forceinline__ void factor_task(const FactorJobDev& J, int local, fl
   for (int v = 0; v < 16; ++v) acc[v] = 0.f;
   contract_tile<LAYOUT, LAYOUT>(J.x, ti * TILE, J.x, tj * TILE, k0, k1, diag, active, lds, acc);
   if (!active) return;
-  float* out = J.slab + (size_t)local * TILE * TILE;
+  float* out = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE;
   const int col = qj * 32 + (lane & 31);
 #pragma unroll
   for (int v = 0; v < 16; ++v) out[(qi * 32 + acc_row(v, lane)) * TILE + col] = acc[v];
 }
 
+
+// One block = one 16-row strip of one 64x64 tile: float4 slab reads (all splits
+// in flight at once), F = beta*F + alpha*sum, then the mirrored strip through LDS.
+// ---------------------------------------------------------------------------
+// Row-major operands with 16-byte-aligned rows (cols, ld multiples of 4): panels
+// arrive by LDS-DMA (global_load_lds_dwordx4) into a 3-slot ring, two stages in
+// flight, counted vmcnt + raw s_barrier (one per stage), no staging VGPRs.  The
+// image is lane-linear [32 rows][64 cols] (256-byte rows, unpadded: the MFMA's
+// ds_read_b32 halves read 32 consecutive dwords, conflict-free).  Chunks past the
+// last real column (bias ones column, tile padding) and rows past the range load
+// from a safe address and are overwritten with their fill value once landed.
+constexpr int GSLOT = 2 * BK * TILE;  // floats per ring slot (A and B panels)
+
+struct GldsPanel {
+  const float* base;
+  int64_t ld, kend;
+  int ch[2];       // this thread's two 16-byte chunks of a panel (0..511)
+  int col[2];      // first column of each chunk
+  bool real[2];    // chunk holds matrix data (else fill)
+  float4 fill[2];  // fill value of a non-real chunk (ones column -> 1)
+  __device__ __forceinline__ void init(const OpDev& op, int col0, int w, int lane, int64_t k_end) {
+    base = op.ptr; ld = op.ld; kend = k_end;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      ch[i] = (w * 2 + i) * 64 + lane;
+      col[i] = col0 + (ch[i] & 15) * 4;
+      real[i] = col[i] < op.cols;
+      float f[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) f[q] = (col[i] + q == op.ones) ? 1.f : 0.f;
+      fill[i] = make_float4(f[0], f[1], f[2], f[3]);
+    }
+  }
+  // issue the two LDS-DMA loads of stage rows [k, k+BK) into `slot` (panel base)
+  __device__ __forceinline__ void issue(int64_t k, float* slot, int w) const {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t row = k + (ch[i] >> 4);
+      const int64_t r = row < kend ? row : kend - 1;
+      const float* src = base + r * ld + (real[i] ? col[i] : 0);
+      __builtin_amdgcn_global_load_lds(src, slot + (w * 2 + i) * 256, 16, 0, 0);
+    }
+  }
+  // after landing: overwrite chunks that must not hold matrix data
+  __device__ __forceinline__ void fixup(int64_t k, float* slot) const {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool okrow = k + (ch[i] >> 4) < kend;
+      if (!real[i] || !okrow) {
+        // inline asm: the explicit vm_wait already covers this lane's DMA; a plain
+        // store would make the compiler drain every in-flight stage (vmcnt(0))
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v v = okrow ? f4v{fill[i].x, fill[i].y, fill[i].z, fill[i].w} : f4v{0.f, 0.f, 0.f, 0.f};
+        const uint32_t addr = (uint32_t)(uintptr_t)(slot + ch[i] * 4);
+        asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ void vm_wait(int n) {
+  // counted waits need immediates
+  if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ void stage_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// NSLOT ring slots (2: one stage in flight, 4 WGs/CU; 3: two in flight, 3 WGs/CU);
+// NACC independent accumulators per wave (k-steps interleaved) to keep back-to-back
+// MFMAs off the 64-cycle dependent-accumulator latency.
+template <int NSLOT, int NACC>
+__device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, int local, float* lds) {
+  const int tiles = J.t * (J.t + 1) / 2;
+  const int split = local / tiles, tile = local - split * tiles;
+  int ti, tj;
+  tri_decode(tile, ti, tj);
+  const int64_t k0 = (int64_t)split * J.chunk;
+  const int64_t k1 = min(J.x.rows, k0 + J.chunk);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int qi = wave >> 1, qj = wave & 1;
+  const bool same = ti == tj;
+  const bool active = !(same && qi < qj);
+  floatx16 acc[NACC];
+#pragma unroll
+  for (int c = 0; c < NACC; ++c)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[c][v] = 0.f;
+
+  if (k1 > k0) {
+    GldsPanel pa, pb;
+    pa.init(J.x, ti * TILE, wave, lane, k1);
+    pb.init(J.x, tj * TILE, wave, lane, k1);
+    const int nst = (int)((k1 - k0 + BK - 1) / BK);
+    const int per = same ? 2 : 4;  // LDS-DMA instructions per stage per thread
+    auto issue = [&](int st) {
+      float* slot = lds + (st % NSLOT) * GSLOT;
+      pa.issue(k0 + (int64_t)st * BK, slot, wave);
+      if (!same) pb.issue(k0 + (int64_t)st * BK, slot + BK * TILE, wave);
+    };
+    issue(0);
+    if (NSLOT == 3 && nst > 1) issue(1);
+    const int h = lane >> 5, rr = lane & 31;
+    for (int st = 0; st < nst; ++st) {
+      // stage st landed (with 3 slots, st+1 may still be in flight)
+      vm_wait(NSLOT == 3 && st + 1 < nst ? per : 0);
+      float* slot = lds + (st % NSLOT) * GSLOT;
+      const int64_t kst = k0 + (int64_t)st * BK;
+      pa.fixup(kst, slot);
+      if (!same) pb.fixup(kst, slot + BK * TILE);
+      stage_barrier();  // stage st visible to all waves; everyone is done with st-1's slot
+      if (st + NSLOT - 1 < nst) issue(st + NSLOT - 1);
+      if (active) {
+        const float* a = slot + h * TILE + qi * 32 + rr;
+        const float* b = slot + (same ? 0 : BK * TILE) + h * TILE + qj * 32 + rr;
+        float av[BK / 2], bv[BK / 2];
+#pragma unroll
+        for (int s2 = 0; s2 < BK / 2; ++s2) {
+          av[s2] = a[2 * s2 * TILE];
+          bv[s2] = b[2 * s2 * TILE];
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < BK / 2; ++s2)
+          acc[s2 % NACC] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s2], bv[s2], acc[s2 % NACC], 0, 0, 0);
+      }
+    }
+  }
+  if (!active) return;
+  float* out = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE;
+  const int col = qj * 32 + (lane & 31);
+#pragma unroll
+  for (int c = 1; c < NACC; ++c)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[0][v] += acc[c][v];
+#pragma unroll
+  for (int v = 0; v < 16; ++v) out[(qi * 32 + acc_row(v, lane)) * TILE + col] = acc[0][v];
+}
+
+// One launch per grouped update: each task takes the LDS-DMA path when its job's
+// operand allows it, else the register-staged path for its layout.
+constexpr int FACTOR_LDS = (4 * PANEL > 2 * GSLOT) ? 4 * PANEL : 2 * GSLOT;
+
 __global__ __launch_bounds__(NTHREADS) void kfac_factor_tiles(FactorArgs args) {
-  __shared__ __attribute__((aligned(16))) float lds[4 * PANEL];
-  const int task = blockIdx.x;
+  __shared__ __attribute__((aligned(16))) float lds[FACTOR_LDS];
+  const int task = xcd_task(blockIdx.x, gridDim.x);
   int j = 0;
   while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
   const FactorJobDev& J = args.job[j];
   const int local = task - J.task_begin;
+  if (J.glds) {
+    factor_task_glds<2, 1>(J, local, lds);
+    return;
+  }
   switch (J.x.layout) {
     case KFAC_ROWMAJOR: factor_task<KFAC_ROWMAJOR>(J, local, lds); break;
     case KFAC_CHANNEL: factor_task<KFAC_CHANNEL>(J, local, lds); break;
@@ -72,8 +225,6 @@ __global__ __launch_bounds__(NTHREADS) void kfac_factor_tiles(FactorArgs args) {
   }
 }
 
-// One block = one 16-row strip of one 64x64 tile: float4 slab reads (all splits
-// in flight at once), F = beta*F + alpha*sum, then the mirrored strip through LDS.
 __global__ __launch_bounds__(NTHREADS) void kfac_factor_reduce(FactorArgs args) {
   __shared__ float strip[16 * LDP];
   const int gtile = blockIdx.x >> 2, s0 = (blockIdx.x & 3) * 16;
@@ -140,13 +291,13 @@ static int factor_n(const kfac_factor_job& j) { return j.x.cols + (j.x.has_ones 
 
 // Split K so that the whole grouped launch has ~4 tasks per CU (256 CUs) but
 // every task still runs >= 256 rows of MFMA work.
-static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans) {
+static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
+                      int64_t target_tasks = 1024) {
   int64_t work = 0;
   for (int i = 0; i < njobs; ++i) {
     const int t = (int)cdiv(factor_n(jobs[i]), TILE);
     work += (int64_t)t * (t + 1) / 2 * cdiv(jobs[i].x.rows, BK);
   }
-  const int64_t target_tasks = 1024;
   int64_t chunk_steps = std::max<int64_t>(8, cdiv(work, target_tasks));  // in BK units
   for (int i = 0; i < njobs; ++i) {
     const int t = (int)cdiv(factor_n(jobs[i]), TILE);
@@ -192,6 +343,9 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
     d.ldF = jb.ldF;
     d.n = factor_n(jb);
     d.t = (int)cdiv(d.n, TILE);
+    d.glds = jb.x.layout == KFAC_ROWMAJOR && jb.x.rows > 0 && jb.x.cols >= 4 &&
+             (jb.x.cols % 4) == 0 && (jb.x.ld % 4) == 0 &&
+             (reinterpret_cast<uintptr_t>(jb.x.ptr) % 16) == 0;
     d.splits = plans[i].splits;
     d.chunk = plans[i].chunk;
     d.slab = reinterpret_cast<float*>(ws + off);
@@ -208,8 +362,8 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
   {
     ProfScope ps(KFAC_PROF_FACTOR_TILES, stream);
     hipLaunchKernelGGL(kfac_factor_tiles, dim3(tasks), dim3(NTHREADS), 0, stream, args);
+    KFAC_CHECK_LAUNCH();
   }
-  KFAC_CHECK_LAUNCH();
   {
     ProfScope ps(KFAC_PROF_FACTOR_REDUCE, stream);
     hipLaunchKernelGGL(kfac_factor_reduce, dim3(tiles * 4), dim3(NTHREADS), 0, stream, args);

@@ -268,6 +268,14 @@ __device__ __forceinline__ int acc_row(int v, int lane) {
 }
 
 // Decode a lower-triangle tile index t -> (ti, tj), ti >= tj.
+// Workgroups are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8), each
+// with its own 4 MB L2.  Hand every XCD a contiguous range of the logical task order
+// so tasks that share operand rows share an L2.  Bijective for any n.
+__device__ __forceinline__ int xcd_task(int b, int n) {
+  const int x = b & 7, s = b >> 3, per = n >> 3, rem = n & 7;
+  return (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + s;
+}
+
 __device__ __forceinline__ void tri_decode(int t, int& ti, int& tj) {
   int i = (int)((sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);
   while ((i + 1) * (i + 2) / 2 <= t) ++i;
