@@ -1,0 +1,59 @@
+"""Turn a profiles/collect.sh run (gpurun_out/prof_<tag>/) into the committed summaries.
+
+    python profiles/summarize.py r01
+
+writes
+  profiles/<tag>/kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
+  profiles/<tag>/pmc_summary.json   per-kernel mean counter value per dispatch, every pass
+  profiles/factor_tiles_pmc.json    HBM bytes per kfac_factor_tiles launch (read by bench.py)
+
+HBM bytes follow MI355X_MICROARCH.md's rocprofv3 section: FETCH_SIZE and WRITE_SIZE
+come from separate passes (KiB units); on gfx950 FETCH_SIZE reports half the bytes of
+a wide (16 B/lane) coalesced read, so it is doubled.  Both the SYRK panel loads
+(global_load_lds_dwordx4 / global_load_dwordx4) and the slab stores are 16 B/lane or
+full 128-B rows.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    return name.split("(")[0].replace("kfac::", "")
+
+
+def main(tag):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    pmc = collections.defaultdict(dict)
+    for f in sorted(glob.glob(os.path.join(src, "pmc_*", "run_counter_collection.csv"))):
+        vals = collections.defaultdict(list)
+        for r in csv.DictReader(open(f)):
+            vals[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
+        for (k, c), v in vals.items():
+            pmc[k][c] = {"mean_per_dispatch": sum(v) / len(v), "dispatches": len(v)}
+    with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
+        json.dump(pmc, f, indent=1, sort_keys=True)
+    t = pmc.get("kfac_factor_tiles", {})
+    if "FETCH_SIZE" in t and "WRITE_SIZE" in t:
+        fetch = t["FETCH_SIZE"]["mean_per_dispatch"] * 1024 * 2  # gfx950: x2 for 16 B/lane reads
+        write = t["WRITE_SIZE"]["mean_per_dispatch"] * 1024
+        out = {"kernel": "kfac_factor_tiles", "tag": tag, "fetch_bytes_per_launch": fetch,
+               "write_bytes_per_launch": write, "hbm_bytes_per_launch": fetch + write,
+               "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->bytes, "
+                       "mean over the bench's launches (15 updates per pass, last batch short)"}
+        with open(os.path.join(ROOT, "profiles", "factor_tiles_pmc.json"), "w") as f:
+            json.dump(out, f, indent=1)
+        print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
