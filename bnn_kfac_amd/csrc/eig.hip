@@ -155,20 +155,285 @@ __global__ __launch_bounds__(NTHREADS) void eig_jacobi_lds(EigArgs args) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// n > 128: Householder tridiagonalisation + Sturm bisection (eigenvalues).
+//
+// eig_tridiag: ONE persistent launch per factor.  G workgroups, row i owned by
+// workgroup i % G (slot i / G), the owned rows kept in LDS for the whole
+// reduction (fp64, symmetrised).  Step k (reflector for column k):
+//   phase A (row-local): p_i = tau * sum_j A[i][j] u_j, partial c = sum p_i u_i
+//   -- grid barrier --
+//   phase B (row-local): w = p - (tau c / 2) u ;  A[i][j] -= u_i w_j + w_i u_j,
+//            then the next column A[i][k+1] (and its partial norm) is published
+//   -- grid barrier --
+// Every workgroup derives the reflector scalars redundantly from the published
+// partials, so the only cross-workgroup data are u / p / two partial vectors.
+// Grid barriers: agent-scope release (one lane, after the workgroup barrier) on
+// an arrival counter, agent-scope acquire poll, bounded spins; a timeout sets
+// `abort` and every workgroup leaves at its next barrier (the launch always
+// drains; the host reports the timeout as info = -1).
+
+struct TriArgs {
+  const float* F;
+  int64_t ldF;
+  int n, G, R;         // rows per workgroup R = ceil(n / G)
+  double* rows_g;      // G x R x n owned rows when they do not fit LDS (else null)
+  double* x;           // 2 x n: published columns (double-buffered by step parity)
+  double* p;           // n
+  double* cpart;       // G
+  double* spart;       // G
+  double* d;           // n: diagonal of T
+  double* e;           // n: off-diagonal of T (e[k] = T[k+1][k])
+  unsigned* bar;       // arrival counter (zeroed before the launch)
+  unsigned* abort;     // timeout flag (zeroed before the launch)
+};
+
+__device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned* abort, unsigned target) {
+  __syncthreads();  // every wave's stores issued and waited (vmcnt 0) before the release
+  __shared__ int bail;
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    int ok = 1;
+    for (unsigned spins = 0;; ++spins) {
+      if (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      if (__hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+          spins > (1u << 22)) {
+        __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    bail = !ok;
+  }
+  __syncthreads();
+  return !bail;
+}
+
+// deterministic: same tree in every workgroup -> bit-identical scalars everywhere
+__device__ __forceinline__ double block_sum(double v, double* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+template <bool LDS_ROWS>
+__global__ __launch_bounds__(NTHREADS) void eig_tridiag(TriArgs a) {
+  extern __shared__ double lds[];  // [u n][w n][rows R x n if LDS_ROWS]
+  __shared__ double red[NTHREADS / 64];
+  const int n = a.n, G = a.G, wg = blockIdx.x, tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  double* uS = lds;
+  double* wS = lds + n;
+  double* rows = LDS_ROWS ? lds + 2 * n : a.rows_g + (size_t)wg * a.R * n;
+  unsigned epoch = 0;
+  auto row_of = [&](int slot) { return slot * G + wg; };
+  auto A = [&](int slot) { return rows + (size_t)slot * n; };
+
+  // load + symmetrise the owned rows; publish column 0 (step 0's x)
+  for (int s = 0; s < a.R; ++s) {
+    const int i = row_of(s);
+    if (i >= n) break;
+    for (int j = tid; j < n; j += NTHREADS)
+      A(s)[j] = 0.5 * ((double)a.F[(int64_t)i * a.ldF + j] + (double)a.F[(int64_t)j * a.ldF + i]);
+  }
+  __syncthreads();
+  {
+    double sig = 0.0;
+    for (int s = tid; s < a.R; s += NTHREADS) {
+      const int i = row_of(s);
+      if (i >= n) continue;
+      const double v = A(s)[0];
+      if (i >= 1) a.x[i] = v;
+      if (i >= 2) sig += v * v;
+      if (i == 0) a.d[0] = v;
+    }
+    sig = block_sum(sig, red);
+    if (tid == 0) a.spart[wg] = sig;
+  }
+  if (!grid_sync(a.bar, a.abort, (++epoch) * G)) return;
+
+  for (int k = 0; k + 2 < n; ++k) {
+    const double* xk = a.x + (size_t)(k & 1) * n;
+    // reflector scalars (every workgroup, redundantly, same order -> same bits)
+    const double sigma = block_sum(tid < G ? a.spart[tid] : 0.0, red);
+    const double alpha = xk[k + 1];
+    double tau = 0.0, u0 = 0.0, beta = alpha;
+    if (sigma > 0.0) {
+      beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+      u0 = alpha - beta;
+      tau = 2.0 / (u0 * u0 + sigma);
+    }
+    if (wg == 0 && tid == 0) a.e[k] = beta;
+    for (int j = k + 1 + tid; j < n; j += NTHREADS) uS[j] = j == k + 1 ? u0 : xk[j];
+    __syncthreads();
+
+    // phase A: p_i = tau * A[i][k+1:] . u, one wave per owned row
+    double cp = 0.0;
+    for (int s = wave; s < a.R; s += NTHREADS / 64) {
+      const int i = row_of(s);
+      if (i >= n) break;
+      if (i <= k) continue;
+      double acc = 0.0;
+      for (int j = k + 1 + lane; j < n; j += 64) acc += A(s)[j] * uS[j];
+      for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+      acc *= tau;
+      if (lane == 0) {
+        a.p[i] = acc;
+        cp += acc * uS[i];
+      }
+    }
+    cp = block_sum(cp, red);
+    if (tid == 0) a.cpart[wg] = cp;
+    if (!grid_sync(a.bar, a.abort, (++epoch) * G)) return;
+
+    // phase B: rank-2 update of the owned trailing rows, publish column k+1
+    const double K = 0.5 * tau * block_sum(tid < G ? a.cpart[tid] : 0.0, red);
+    for (int j = k + 1 + tid; j < n; j += NTHREADS) wS[j] = a.p[j] - K * uS[j];
+    __syncthreads();
+    for (int s = 0; s < a.R; ++s) {
+      const int i = row_of(s);
+      if (i >= n) break;
+      if (i <= k) continue;
+      const double ui = uS[i], wi = wS[i];
+      for (int j = k + 1 + tid; j < n; j += NTHREADS) A(s)[j] -= ui * wS[j] + wi * uS[j];
+    }
+    __syncthreads();
+    double* xn = a.x + (size_t)((k + 1) & 1) * n;
+    double sig = 0.0;
+    for (int s = tid; s < a.R; s += NTHREADS) {
+      const int i = row_of(s);
+      if (i >= n) continue;
+      const double v = A(s)[k + 1];
+      if (i == k + 1) a.d[k + 1] = v;
+      if (i >= k + 2) xn[i] = v;
+      if (i >= k + 3) sig += v * v;
+    }
+    sig = block_sum(sig, red);
+    if (tid == 0) a.spart[wg] = sig;
+    if (!grid_sync(a.bar, a.abort, (++epoch) * G)) return;
+  }
+  // tail: T[n-1][n-1] and T[n-1][n-2] from their owner
+  if (n >= 2 && tid == 0) {
+    for (int s = 0; s < a.R; ++s) {
+      if (row_of(s) == n - 1) {
+        a.d[n - 1] = A(s)[n - 1];
+        a.e[n - 2] = A(s)[n - 2];
+      }
+    }
+  }
+}
+
+// Eigenvalues of the symmetric tridiagonal (d, e) by Sturm-count bisection, one
+// thread per eigenvalue index (k-th smallest -> ascending order for free).
+__global__ __launch_bounds__(NTHREADS) void eig_bisect(const double* d, const double* e, int n,
+                                                       double* evals, const unsigned* abort, int* info) {
+  const int k = blockIdx.x * NTHREADS + threadIdx.x;
+  if (k == 0 && info) *info = *abort ? -1 : 0;
+  if (k >= n) return;
+  double lo = 0.0, hi = 0.0, emax2 = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double r = (i > 0 ? fabs(e[i - 1]) : 0.0) + (i + 1 < n ? fabs(e[i]) : 0.0);
+    lo = i ? fmin(lo, d[i] - r) : d[i] - r;
+    hi = i ? fmax(hi, d[i] + r) : d[i] + r;
+    if (i + 1 < n) emax2 = fmax(emax2, e[i] * e[i]);
+  }
+  const double pivmin = 1e-290 * fmax(1.0, emax2);
+  const double span = fmax(fabs(lo), fabs(hi));
+  lo -= 2.2e-16 * span + pivmin;
+  hi += 2.2e-16 * span + pivmin;
+  for (int it = 0; it < 200; ++it) {
+    const double mid = 0.5 * (lo + hi);
+    if (hi - lo <= 2.0 * 2.2e-16 * fmax(fabs(lo), fabs(hi)) + pivmin || mid == lo || mid == hi) break;
+    // count of eigenvalues < mid (LDL^T inertia)
+    int cnt = 0;
+    double q = d[0] - mid;
+    if (fabs(q) < pivmin) q = -pivmin;
+    cnt += q < 0.0;
+    for (int i = 1; i < n; ++i) {
+      q = d[i] - mid - e[i - 1] * e[i - 1] / q;
+      if (fabs(q) < pivmin) q = -pivmin;
+      cnt += q < 0.0;
+    }
+    if (cnt > k) hi = mid; else lo = mid;
+  }
+  evals[k] = 0.5 * (lo + hi);
+}
+
 }  // namespace kfac
 
 using namespace kfac;
 
+// n > EIG_LDS_MAX: tridiagonalisation plan (grid, rows per workgroup, row storage)
+struct TriPlan {
+  int G, R;
+  bool lds_rows;
+  size_t shmem, ws;
+};
+constexpr size_t TRI_LDS_BUDGET = 150 * 1024;
+
+static TriPlan tri_plan(int n) {
+  TriPlan p;
+  p.G = std::min(256, std::max(1, (n + 7) / 8));
+  p.R = (n + p.G - 1) / p.G;
+  p.lds_rows = (size_t)(2 + p.R) * n * sizeof(double) <= TRI_LDS_BUDGET;
+  p.shmem = (size_t)(p.lds_rows ? 2 + p.R : 2) * n * sizeof(double);
+  p.ws = 256                                                    // bar, abort (+pad)
+         + align_up((size_t)2 * n * sizeof(double), 256)        // x
+         + 3 * align_up((size_t)n * sizeof(double), 256)        // p, d, e
+         + 2 * align_up(256 * sizeof(double), 256)              // cpart, spart
+         + (p.lds_rows ? 0 : align_up((size_t)p.G * p.R * n * sizeof(double), 256));
+  return p;
+}
+
+static int tridiag_eigvals(const kfac_eig_job& j, char* ws, int32_t* info, hipStream_t stream) {
+  const TriPlan pl = tri_plan(j.n);
+  if (pl.shmem > TRI_LDS_BUDGET) return KFAC_EINVAL;
+  TriArgs t{};
+  t.F = j.F; t.ldF = j.ldF; t.n = j.n; t.G = pl.G; t.R = pl.R;
+  t.bar = reinterpret_cast<unsigned*>(ws);
+  t.abort = t.bar + 1;
+  char* q = ws + 256;
+  t.x = reinterpret_cast<double*>(q); q += align_up((size_t)2 * j.n * sizeof(double), 256);
+  t.p = reinterpret_cast<double*>(q); q += align_up((size_t)j.n * sizeof(double), 256);
+  t.d = reinterpret_cast<double*>(q); q += align_up((size_t)j.n * sizeof(double), 256);
+  t.e = reinterpret_cast<double*>(q); q += align_up((size_t)j.n * sizeof(double), 256);
+  t.cpart = reinterpret_cast<double*>(q); q += align_up(256 * sizeof(double), 256);
+  t.spart = reinterpret_cast<double*>(q); q += align_up(256 * sizeof(double), 256);
+  t.rows_g = pl.lds_rows ? nullptr : reinterpret_cast<double*>(q);
+  if (hipMemsetAsync(ws, 0, 16, stream) != hipSuccess) return KFAC_ELAUNCH;
+  const void* fn = pl.lds_rows ? reinterpret_cast<const void*>(&eig_tridiag<true>)
+                               : reinterpret_cast<const void*>(&eig_tridiag<false>);
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.shmem) != hipSuccess)
+    return KFAC_ELAUNCH;
+  void* kargs[] = {&t};
+  // cooperative: the runtime rejects a grid that cannot be co-resident (no deadlock)
+  if (hipLaunchCooperativeKernel(fn, dim3(pl.G), dim3(NTHREADS), kargs, (unsigned)pl.shmem, stream) !=
+      hipSuccess)
+    return KFAC_ELAUNCH;
+  hipLaunchKernelGGL(eig_bisect, dim3((j.n + NTHREADS - 1) / NTHREADS), dim3(NTHREADS), 0, stream,
+                     t.d, t.e, j.n, j.evals, t.abort, info);
+  KFAC_CHECK_LAUNCH();
+  return KFAC_OK;
+}
+
 extern "C" size_t kfac_eig_workspace_bytes(const kfac_eig_job* jobs, int njobs) {
   if (!jobs || njobs <= 0) return 0;
-  size_t best = 0;
-  for (int g = 0; g < njobs; g += EMAXJ) {
-    size_t tot = 0;
-    for (int i = g; i < std::min(njobs, g + EMAXJ); ++i)
-      tot += align_up((size_t)jobs[i].n * jobs[i].n * sizeof(double), 256);
-    best = std::max(best, tot);
+  // small factors run grouped (V per job); large ones one at a time (stream-ordered reuse)
+  size_t best = 0, tot = 0;
+  int in_group = 0;
+  for (int i = 0; i < njobs; ++i) {
+    if (jobs[i].n > EIG_LDS_MAX) {
+      best = std::max(best, tri_plan(jobs[i].n).ws);
+      continue;
+    }
+    if (in_group == EMAXJ) { best = std::max(best, tot); tot = 0; in_group = 0; }
+    tot += align_up((size_t)jobs[i].n * jobs[i].n * sizeof(double), 256);
+    ++in_group;
   }
-  return best;
+  return std::max(best, tot);
 }
 
 extern "C" int kfac_syev(const kfac_eig_job* jobs, int njobs, void* workspace, size_t workspace_bytes,
@@ -177,24 +442,41 @@ extern "C" int kfac_syev(const kfac_eig_job* jobs, int njobs, void* workspace, s
   for (int i = 0; i < njobs; ++i) {
     const kfac_eig_job& j = jobs[i];
     if (!j.F || !j.evals || j.n <= 0 || j.ldF < j.n || (j.evecs && j.ldv < j.n)) return KFAC_EINVAL;
-    if (j.n > EIG_LDS_MAX) return KFAC_EINVAL;  // larger factors: blocked solver (not yet)
+    // large factors: eigenvalues (tridiagonal route); eigenvectors not yet
+    if (j.n > EIG_LDS_MAX && j.evecs) return KFAC_EINVAL;
   }
   if (workspace_bytes < kfac_eig_workspace_bytes(jobs, njobs)) return KFAC_EWORKSPACE;
-  for (int g = 0; g < njobs; g += EMAXJ) {
-    EigArgs args{};
-    args.njobs = std::min(EMAXJ, njobs - g);
-    char* ws = (char*)workspace;
-    for (int i = 0; i < args.njobs; ++i) {
-      const kfac_eig_job& j = jobs[g + i];
-      EigJobDev& d = args.job[i];
-      d.F = j.F; d.ldF = j.ldF; d.n = j.n; d.evals = j.evals; d.evecs = j.evecs; d.ldv = j.ldv;
-      d.V = j.evecs ? reinterpret_cast<double*>(ws) : nullptr;
-      ws += align_up((size_t)j.n * j.n * sizeof(double), 256);
-      d.info = info ? info + g + i : nullptr;
-    }
-    hipLaunchKernelGGL(eig_jacobi_lds, dim3(args.njobs), dim3(NTHREADS), 0, (hipStream_t)stream,
-                       args);
+  hipStream_t st = (hipStream_t)stream;
+  EigArgs args{};
+  char* ws = (char*)workspace;
+  auto flush = [&]() -> int {
+    if (args.njobs == 0) return KFAC_OK;
+    hipLaunchKernelGGL(eig_jacobi_lds, dim3(args.njobs), dim3(NTHREADS), 0, st, args);
     KFAC_CHECK_LAUNCH();
+    args = EigArgs{};
+    ws = (char*)workspace;
+    return KFAC_OK;
+  };
+  for (int i = 0; i < njobs; ++i) {
+    const kfac_eig_job& j = jobs[i];
+    if (j.n > EIG_LDS_MAX) {
+      int rc = flush();  // the small group owns the workspace until its launch is queued
+      if (rc != KFAC_OK) return rc;
+      rc = tridiag_eigvals(j, (char*)workspace, info ? info + i : nullptr, st);
+      if (rc != KFAC_OK) return rc;
+      continue;
+    }
+    if (args.njobs == EMAXJ) {
+      const int rc = flush();
+      if (rc != KFAC_OK) return rc;
+    }
+    EigJobDev& d = args.job[args.njobs++];
+    d.F = j.F; d.ldF = j.ldF; d.n = j.n; d.evals = j.evals; d.evecs = j.evecs; d.ldv = j.ldv;
+    d.V = j.evecs ? reinterpret_cast<double*>(ws) : nullptr;
+    ws += align_up((size_t)j.n * j.n * sizeof(double), 256);
+    d.info = info ? info + i : nullptr;
   }
+  const int rc = flush();
+  if (rc != KFAC_OK) return rc;
   return KFAC_OK;
 }

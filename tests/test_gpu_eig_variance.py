@@ -113,3 +113,76 @@ def test_regression_variance_golden(hip_device):
         out, v = kron_quadform(terms, lower=False, per_term=True)
         np.testing.assert_allclose(v.cpu().numpy()[:, 0], g["v"][j], rtol=2e-3, atol=1e-7)
         np.testing.assert_allclose(float(out[0]) ** 0.5 + sigma, g["std"][j], rtol=1e-4)
+
+
+# ---------------------------------------------------------------- n > 128: tridiagonal route
+def _eigvals_dev(F, dev):
+    from bnn_kfac_amd.utilities import symeig
+    (ev, _), = symeig([_t(F, dev)])
+    return ev.cpu().numpy()
+
+
+@pytest.mark.parametrize("n,kind", [(129, "sym"), (200, "spd"), (785, "spd"), (1000, "sym"),
+                                    (2048, "spd")])
+def test_eigvals_large(hip_device, n, kind):
+    """Householder tridiagonalisation (LDS-resident rows; global rows at 2048) +
+    Sturm bisection vs LAPACK eigvalsh in fp64 on the same fp32 matrix."""
+    rng = np.random.default_rng(n)
+    X = rng.standard_normal((n, n)).astype(np.float32)
+    F = (X + X.T) if kind == "sym" else (X @ X.T / n + 1e-3 * np.eye(n, dtype=np.float32))
+    F = F.astype(np.float32)
+    ev = _eigvals_dev(F, hip_device)
+    want = np.linalg.eigvalsh(F.astype(np.float64))
+    scale = np.abs(want).max()
+    assert np.all(np.diff(ev) >= 0)  # ascending, like eigvalsh / torch.symeig
+    np.testing.assert_allclose(ev, want, rtol=1e-9, atol=1e-11 * scale)
+
+
+@pytest.mark.parametrize("kind", ["identity", "diagonal", "repeated"])
+def test_eigvals_large_structured(hip_device, kind):
+    """Zero sub-columns (no reflection needed) and exactly repeated eigenvalues."""
+    n = 300
+    rng = np.random.default_rng(1)
+    if kind == "identity":
+        F = 3.0 * np.eye(n)
+    elif kind == "diagonal":
+        F = np.diag(rng.standard_normal(n))
+    else:
+        Q, _ = np.linalg.qr(rng.standard_normal((n, n)))
+        F = (Q * np.repeat([1.0, 2.0, 5.0], n // 3)) @ Q.T
+    F = F.astype(np.float32)
+    ev = _eigvals_dev(F, hip_device)
+    want = np.linalg.eigvalsh(F.astype(np.float64))
+    np.testing.assert_allclose(ev, want, rtol=1e-9, atol=1e-11 * np.abs(want).max())
+
+
+def test_get_eigenvalues_mlp_golden(hip_device):
+    """utilities.py:120-141 at the MLP's sizes (A 785^2 and 129^2 take the large path):
+    the device factors' eigenvalues vs the reference's (golden A1_eig: eigvalsh of the
+    reference's own fp32 A1) — rtol 1e-5 of the spectrum."""
+    from bnn_kfac_amd.curvatures import KFAC
+    from bnn_kfac_amd.utilities import get_eigenvalues, symeig
+    from test_oracle_golden import mlp_batches
+    g = golden("g1_mlp.npz")
+    net = nn.Sequential(nn.Linear(784, 128), nn.ReLU(), nn.Linear(128, 10)).to(hip_device)
+    kfac = KFAC(net)
+    for B, a1, g1, a2, g2 in mlp_batches():
+        kfac.record[net[0]] = [_t(a1, hip_device), _t(g1, hip_device)]
+        kfac.record[net[2]] = [_t(a2, hip_device), _t(g2, hip_device)]
+        kfac.update(batch_size=B)
+    A1, G1 = kfac.state[net[0]]
+    A2, G2 = kfac.state[net[2]]
+    ev_a1 = symeig([A1])[0][0].cpu().numpy()
+    np.testing.assert_allclose(ev_a1, g["A1_eig"], rtol=1e-5, atol=1e-5 * np.abs(g["A1_eig"]).max())
+    ev = get_eigenvalues([[A1, G1], [A2, G2]]).cpu().numpy()
+    want = O.get_eigenvalues([(A1.cpu().numpy(), G1.cpu().numpy()),
+                              (A2.cpu().numpy(), G2.cpu().numpy())])
+    np.testing.assert_allclose(ev, want, rtol=1e-5, atol=1e-6 * np.abs(want).max())
+
+
+def test_large_eigenvectors_not_supported_yet(hip_device):
+    from bnn_kfac_amd import _native as N
+    from bnn_kfac_amd.utilities import symeig
+    F = torch.eye(200, device=hip_device)
+    with pytest.raises(N.NativeError):
+        symeig([F], eigenvectors=True)
