@@ -11,12 +11,12 @@
 //
 // Blocked over 64x64 fp64 tiles; every launch is grouped over ALL factors:
 //   inv_build       R' = P R P (damped, symmetrised, identity padded); Z = 0
-//   inv_update(-1)  factor tile (0,0): X[0][0] = chol(R'[0][0])^{-1}
-//   for k = 0..T-1:
-//     inv_panel(k)  C[i][k] = R'[i][k] X[k][k]^T          (i > k)
-//                   X[k][j] = X[k][k] Z[k][j]              (j < k)
-//     inv_update(k) R'[i][j] -= C[i][k] C[j][k]^T          (i >= j > k)
-//                   Z[i][j]  -= C[i][k] X[k][j]            (i > k >= j)
+//   inv_step(-1)    factor tile (0,0): X[0][0] = chol(R'[0][0])^{-1}
+//   for k = 0..T-1: inv_step(k), ONE launch per step, the panel folded in:
+//                   C_i = R'[i][k] X[k][k]^T formed where needed (never stored)
+//                   R'[i][j] -= C_i C_j^T                 (i >= j > k)
+//                   Z[i][j]  -= C_i X[k][k] Z[k][j]        (i > k >= j)
+//                   X[k][j]   = X[k][k] Z[k][j] -> W[k][j] (final, j < k)
 //                   and the block owning (k+1,k+1) factors it right after its
 //                   update -> X[k+1][k+1] (one factorisation per step).
 //   [inv_xtx]       Y = X^T X (only for the full-inverse output)
@@ -299,99 +299,144 @@ __global__ __launch_bounds__(NTHREADS) void inv_build(InvArgs args) {
   }
 }
 
-// ------------------------------------------------------------------- update k
-__global__ __launch_bounds__(NTHREADS) void inv_update(InvArgs args) {
-  __shared__ __attribute__((aligned(16))) double A[NB * DP];
-  __shared__ __attribute__((aligned(16))) double B[NB * DP];
-  __shared__ __attribute__((aligned(16))) double Y[NB * DP];
+// acc (gemm64 layout) -> LDS tile
+__device__ __forceinline__ void store_acc_lds(double* S, const doublex4 (&acc)[4]) {
+  const int w = threadIdx.x >> 6, col = threadIdx.x & 15;
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) S[(16 * w + acc_row64(v)) * DP + 16 * jb + col] = acc[jb][v];
+}
+
+// C_i = R'[i][k] X[k][k]^T into Sdst (Xkk already in LDS; Sdst holds R'[i][k] on entry)
+__device__ __forceinline__ void panel_tile_lds(double* Sdst, const double* Xkk) {
+  doublex4 acc[4];
+  gemm64<true>(Sdst, Xkk, acc);
+  __syncthreads();  // every wave done reading R'[i][k] before it is overwritten
+  store_acc_lds(Sdst, acc);
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------- step k
+// One launch per elimination step (the panel is folded in: every workgroup forms
+// the panel blocks it needs, C[i][k] = R'[i][k] X[k][k]^T, itself; C is never
+// stored — column k is dead after step k).
+//   k = -1        : factor tile (0,0)                      -> X[0][0]
+//   k <= T-2      : trailing  R'[i][j] -= C_i C_j^T        (i >= j > k)
+//                   the (k+1,k+1) workgroup then factors   -> X[k+1][k+1]
+//                   Z[i][j] -= C_i B,  B = X[k][k] (j = k) or X[k][k] Z[k][j] (j < k)
+//                   row k+1's Z workgroups also store X[k][j] = X[k][k] Z[k][j]
+//                   (final) into W[k][j], dead since step j (Z[k][j] stays intact
+//                   for the other readers of this launch)
+//   k = T-1       : X[k][j] = X[k][k] Z[k][j] -> W[k][j]   (j < k)
+// Final inverse X: diagonal tiles in X, strictly-lower tiles in W (x_tile()).
+// trailing tile (i, j), i >= j > k: R'[i][j] -= C_i C_j^T.  Returns true for the
+// (k+1, k+1) workgroup, which then holds the updated diagonal tile in S0.
+__device__ __forceinline__ bool step_trailing(const InvJobDev& J, int k, int local, double* S0,
+                                              double* S1, double* S2) {
+  int a, b;
+  tri_decode(local, a, b);
+  const int i = k + 1 + a, j = k + 1 + b;
+  load_tile(S0, tile_ptr(J.X, J.Np, k, k), J.Np);
+  load_tile(S1, tile_ptr(J.W, J.Np, i, k), J.Np);
+  if (j != i) load_tile(S2, tile_ptr(J.W, J.Np, j, k), J.Np);
+  __syncthreads();
+  panel_tile_lds(S1, S0);              // C_i
+  if (j != i) panel_tile_lds(S2, S0);  // C_j
+  doublex4 acc[4];
+  gemm64<true>(S1, j != i ? S2 : S1, acc);
+  if (!(i == k + 1 && j == k + 1)) {
+    store_acc_global(tile_ptr(J.W, J.Np, i, j), J.Np, acc, -1.0, true);
+    return false;
+  }
+  // the updated diagonal tile is consumed right here (never written back)
+  __syncthreads();
+  load_tile(S0, tile_ptr(J.W, J.Np, i, i), J.Np);
+  __syncthreads();
+  const int w = threadIdx.x >> 6, col = threadIdx.x & 15;
+#pragma unroll
+  for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) S0[(16 * w + acc_row64(v)) * DP + 16 * b4 + col] -= acc[b4][v];
+  __syncthreads();
+  return true;
+}
+
+// Z tile (i, j), i > k >= j: Z[i][j] -= C_i B, B = X[k][k] (j = k) or
+// X[k][k] Z[k][j] (j < k; row k+1's workgroup also stores it as the final X[k][j]).
+__device__ __forceinline__ void step_z(const InvJobDev& J, int k, int u, double* S0, double* S1,
+                                       double* S2) {
+  const int i = k + 1 + u / (k + 1), j = u % (k + 1);
+  load_tile(S0, tile_ptr(J.X, J.Np, k, k), J.Np);
+  load_tile(S1, tile_ptr(J.W, J.Np, i, k), J.Np);
+  if (j < k) load_tile(S2, tile_ptr(J.X, J.Np, k, j), J.Np);
+  __syncthreads();
+  panel_tile_lds(S1, S0);  // C_i
+  doublex4 acc[4];
+  const double* Bm = S0;
+  if (j < k) {
+    gemm64<false>(S0, S2, acc);
+    __syncthreads();
+    store_acc_lds(S2, acc);
+    if (i == k + 1) store_acc_global(tile_ptr(J.W, J.Np, k, j), J.Np, acc, 1.0, false);
+    __syncthreads();
+    Bm = S2;
+  }
+  gemm64<false>(S1, Bm, acc);
+  store_acc_global(tile_ptr(J.X, J.Np, i, j), J.Np, acc, -1.0, true);
+}
+
+// last row of X (k = T-1): X[k][j] = X[k][k] Z[k][j] -> W[k][j]
+__device__ __forceinline__ void step_last_row(const InvJobDev& J, int k, int j, double* S0,
+                                              double* S1) {
+  load_tile(S0, tile_ptr(J.X, J.Np, k, k), J.Np);
+  load_tile(S1, tile_ptr(J.X, J.Np, k, j), J.Np);
+  __syncthreads();
+  doublex4 acc[4];
+  gemm64<false>(S0, S1, acc);
+  store_acc_global(tile_ptr(J.W, J.Np, k, j), J.Np, acc, 1.0, false);
+}
+
+__global__ __launch_bounds__(NTHREADS) void inv_step(InvArgs args) {
+  __shared__ __attribute__((aligned(16))) double S0[NB * DP];
+  __shared__ __attribute__((aligned(16))) double S1[NB * DP];
+  __shared__ __attribute__((aligned(16))) double S2[NB * DP];
   __shared__ double dg[NB + 352];  // pivots + elimination broadcast buffers
   const int jb = find_job(args, blockIdx.x);
   const InvJobDev& J = args.job[jb];
   const int k = args.step, T = J.T;
   const int local = blockIdx.x - args.begin[jb];
   const int nTrail = (T - k - 1) * (T - k) / 2;
-  if (k < 0 || local < nTrail) {
-    int i = k + 1, j = k + 1;
-    if (k >= 0) {
-      int a, b;
-      tri_decode(local, a, b);
-      i = k + 1 + a;
-      j = k + 1 + b;
-    }
-    const bool factor = (i == k + 1 && j == k + 1);
-    doublex4 acc[4];
-    if (k >= 0) {
-      load_tile(A, tile_ptr(J.W, J.Np, i, k), J.Np);
-      load_tile(B, tile_ptr(J.W, J.Np, j, k), J.Np);
-      __syncthreads();
-      gemm64<true>(A, B, acc);
-    }
-    if (!factor) {
-      store_acc_global(tile_ptr(J.W, J.Np, i, j), J.Np, acc, -1.0, true);
-      return;
-    }
-    // the updated diagonal tile is consumed right here (never written back)
+  if (k < 0) {  // first diagonal tile
+    load_tile(S0, tile_ptr(J.W, J.Np, 0, 0), J.Np);
     __syncthreads();
-    load_tile(A, tile_ptr(J.W, J.Np, i, i), J.Np);
-    __syncthreads();
-    if (k >= 0) {
-      const int w = threadIdx.x >> 6, col = threadIdx.x & 15;
-#pragma unroll
-      for (int b4 = 0; b4 < 4; ++b4)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) A[(16 * w + acc_row64(v)) * DP + 16 * b4 + col] -= acc[b4][v];
-      __syncthreads();
-    }
-    diag_factor(A, Y, dg);
-    if (threadIdx.x == 0 && J.info) {
-      for (int c = 0; c < NB; ++c) {
-        const int g = i * NB + c;
-        if (g < J.n && !(dg[c] > 0.0)) {
-          atomicCAS(J.info, 0, g + 1);
-          break;
-        }
-      }
-    }
-    store_tile(tile_ptr(J.X, J.Np, i, i), Y, J.Np);
+  } else if (k == T - 1) {
+    step_last_row(J, k, local, S0, S1);
+    return;
+  } else if (local >= nTrail) {
+    step_z(J, k, local - nTrail, S0, S1, S2);
+    return;
+  } else if (!step_trailing(J, k, local, S0, S1, S2)) {
     return;
   }
-  // Z[i][j] -= C[i][k] X[k][j]   (i > k >= j)
-  const int u = local - nTrail;
-  const int i = k + 1 + u / (k + 1), j = u % (k + 1);
-  load_tile(A, tile_ptr(J.W, J.Np, i, k), J.Np);
-  load_tile(B, tile_ptr(J.X, J.Np, k, j), J.Np);
-  __syncthreads();
-  doublex4 acc[4];
-  gemm64<false>(A, B, acc);
-  store_acc_global(tile_ptr(J.X, J.Np, i, j), J.Np, acc, -1.0, true);
+  // the one diagonal factorisation of this step (single call site: stays inlined)
+  const int d = k + 1;
+  diag_factor(S0, S1, dg);
+  if (threadIdx.x == 0 && J.info) {
+    for (int c = 0; c < NB; ++c) {
+      const int g = d * NB + c;
+      if (g < J.n && !(dg[c] > 0.0)) {
+        atomicCAS(J.info, 0, g + 1);
+        break;
+      }
+    }
+  }
+  store_tile(tile_ptr(J.X, J.Np, d, d), S1, J.Np);
 }
 
-// -------------------------------------------------------------------- panel k
-__global__ __launch_bounds__(NTHREADS) void inv_panel(InvArgs args) {
-  __shared__ __attribute__((aligned(16))) double A[NB * DP];
-  __shared__ __attribute__((aligned(16))) double Xk[NB * DP];
-  const int jb = find_job(args, blockIdx.x);
-  const InvJobDev& J = args.job[jb];
-  const int k = args.step, T = J.T;
-  const int local = blockIdx.x - args.begin[jb];
-  const int nC = T - k - 1;
-  load_tile(Xk, tile_ptr(J.X, J.Np, k, k), J.Np);
-  doublex4 acc[4];
-  if (local < nC) {  // C[i][k] = R'[i][k] X[k][k]^T
-    const int i = k + 1 + local;
-    double* t = tile_ptr(J.W, J.Np, i, k);
-    load_tile(A, t, J.Np);
-    __syncthreads();
-    gemm64<true>(A, Xk, acc);
-    store_acc_global(t, J.Np, acc, 1.0, false);
-  } else {           // X[k][j] = X[k][k] Z[k][j]
-    const int j = local - nC;
-    double* t = tile_ptr(J.X, J.Np, k, j);
-    load_tile(A, t, J.Np);
-    __syncthreads();
-    gemm64<false>(Xk, A, acc);
-    store_acc_global(t, J.Np, acc, 1.0, false);
-  }
+// final inverse X tile (a >= b): strictly-lower tiles live in W (see inv_step)
+__device__ __forceinline__ const double* x_tile(const InvJobDev& J, int a, int b) {
+  return tile_ptr(a > b ? J.W : J.X, J.Np, a, b);
 }
 
 // Y[a][b] = sum_{m >= a} X[m][a]^T X[m][b]   (lower tiles, a >= b)
@@ -407,8 +452,8 @@ __global__ __launch_bounds__(NTHREADS) void inv_xtx(InvArgs args) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = doublex4{0.0, 0.0, 0.0, 0.0};
   for (int m = a; m < J.T; ++m) {
-    load_tile(A, tile_ptr(J.X, J.Np, m, a), J.Np);  // read transposed below
-    load_tile(B, tile_ptr(J.X, J.Np, m, b), J.Np);
+    load_tile(A, x_tile(J, m, a), J.Np);  // read transposed below
+    load_tile(B, x_tile(J, m, b), J.Np);
     __syncthreads();
     const int i = lane & 15, kk = lane >> 4;
 #pragma unroll
@@ -435,7 +480,8 @@ __global__ __launch_bounds__(NTHREADS) void inv_out(InvArgs args) {
     if (i >= n || c >= n) continue;
     double v;
     if (J.kind == KFAC_OUT_INV_CHOL) {
-      v = (i >= c) ? J.X[(int64_t)(n - 1 - c) * J.Np + (n - 1 - i)] : 0.0;
+      const int r = n - 1 - c, q = n - 1 - i;  // L[i][c] = X[r][q], r >= q
+      v = (i >= c) ? ((r >> 6) > (q >> 6) ? J.W : J.X)[(int64_t)r * J.Np + q] : 0.0;
     } else {
       const int a = n - 1 - i, b = n - 1 - c;
       v = (a >= b) ? J.Tm[(int64_t)a * J.Np + b] : J.Tm[(int64_t)b * J.Np + a];
@@ -498,15 +544,12 @@ static int invert_group(const kfac_invert_job* jobs, int njobs, char* ws, int32_
   }
   rc = launch(inv_build, args, [](const InvJobDev& d) { return d.T * (d.T + 1) / 2; }, s);
   if (rc) return rc;
-  args.step = -1;
-  rc = launch(inv_update, args, [](const InvJobDev&) { return 1; }, s);
-  if (rc) return rc;
-  for (int k = 0; k < Tmax; ++k) {
+  for (int k = -1; k < Tmax; ++k) {
     args.step = k;
-    rc = launch(inv_panel, args, [k](const InvJobDev& d) { return k < d.T ? d.T - 1 : 0; }, s);
-    if (rc) return rc;
-    rc = launch(inv_update, args, [k](const InvJobDev& d) {
-      return k + 1 < d.T ? (d.T - k - 1) * (d.T - k) / 2 + (d.T - k - 1) * (k + 1) : 0;
+    rc = launch(inv_step, args, [k](const InvJobDev& d) {
+      if (k < 0) return 1;
+      if (k + 1 < d.T) return (d.T - k - 1) * (d.T - k) / 2 + (d.T - k - 1) * (k + 1);
+      return k + 1 == d.T ? k : 0;  // last row of X
     }, s);
     if (rc) return rc;
   }
