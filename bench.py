@@ -36,64 +36,91 @@ MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md, chi
 DAMPING = (0.2 ** 2, 200)     # invert(std**2, N), classification_ll_block.py:72-73,106
 
 
-def layer_dims(config):
-    """(d_in, d_out) of the KFAC'd Linear layers."""
-    if config == "mlp":
-        return [(784, 128), (128, 10)]
-    if config == "wide":
-        return [(784, 4096), (4096, 4096), (4096, 10)]
-    raise ValueError(config)
+class Layer:
+    """A KFAC'd layer of a bench config: Linear (d_in, d_out) or Conv2d
+    (C_in, C_out, kernel, padding, stride, H_in) with square images."""
+
+    def __init__(self, kind, *p):
+        self.kind = kind
+        if kind == "linear":
+            d_in, d_out = p
+            self.in_shape, self.out_shape, self.L = (d_in,), (d_out,), 1
+            self.nA, self.nG = d_in + 1, d_out
+        else:
+            C, Co, k, pad, st, H = p
+            Ho = (H + 2 * pad - k) // st + 1
+            self.k, self.pad, self.stride = k, pad, st
+            self.in_shape, self.out_shape, self.L = (C, H, H), (Co, Ho, Ho), Ho * Ho
+            self.nA, self.nG = C * k * k + 1, Co
 
 
-def flops_per_image(dims):
-    """Algorithmic SYRK work: sum_layers n_A(n_A+1) + n_G(n_G+1) (lower triangle incl.
-    the bias ones column)."""
-    return sum((a + 1) * (a + 2) + g * (g + 1) for a, g in dims)
+CONFIGS = {
+    "mlp": [Layer("linear", 784, 128), Layer("linear", 128, 10)],
+    "wide": [Layer("linear", 784, 4096), Layer("linear", 4096, 4096), Layer("linear", 4096, 10)],
+    # LeNet-5: conv1 1->6 k5 p2, pool, conv2 6->16 k5, pool, fc 400-120-84-10 (SURVEY §8d C3)
+    "lenet": [Layer("conv", 1, 6, 5, 2, 1, 28), Layer("conv", 6, 16, 5, 0, 1, 14),
+              Layer("linear", 400, 120), Layer("linear", 120, 84), Layer("linear", 84, 10)],
+}
+NAMES = {"mlp": "MLP 784-128-10", "wide": "Wide MLP 784-4096-4096-10", "lenet": "LeNet-5"}
 
 
-def bytes_per_image(dims):
-    return sum(4 * (a + g) for a, g in dims)
+def flops_per_image(layers):
+    """Algorithmic SYRK work: sum_layers L [n_A(n_A+1) + n_G(n_G+1)] (lower triangle incl.
+    the bias ones column): MLP 650,402; LeNet-5 3,110,740."""
+    return sum(l.L * (l.nA * (l.nA + 1) + l.nG * (l.nG + 1)) for l in layers)
+
+
+def bytes_per_image(layers):
+    return sum(4 * (int(np.prod(l.in_shape)) + int(np.prod(l.out_shape))) for l in layers)
 
 
 def build_model(config, device):
-    """Random-init MLP of the configured shape (default torch init, seed 0)."""
+    """Random-init model of the configured shape (default torch init, seed 0)."""
     torch.manual_seed(0)
-    mods, dims = [], layer_dims(config)
-    for i, (d_in, d_out) in enumerate(dims):
-        mods.append(torch.nn.Linear(d_in, d_out))
-        if i + 1 < len(dims):
-            mods.append(torch.nn.ReLU())
-    return torch.nn.Sequential(*mods).to(device)
+    nn = torch.nn
+    if config == "lenet":
+        net = nn.Sequential(nn.Conv2d(1, 6, 5, padding=2), nn.ReLU(), nn.MaxPool2d(2),
+                            nn.Conv2d(6, 16, 5), nn.ReLU(), nn.MaxPool2d(2), nn.Flatten(),
+                            nn.Linear(400, 120), nn.ReLU(), nn.Linear(120, 84), nn.ReLU(),
+                            nn.Linear(84, 10))
+        return net.to(device)
+    mods, layers = [], CONFIGS[config]
+    for i, l in enumerate(layers):
+        mods.append(nn.Linear(l.in_shape[0], l.out_shape[0]))
+        if i + 1 < len(layers):
+            mods.append(nn.ReLU())
+    return nn.Sequential(*mods).to(device)
 
 
-def synthetic_records(dims, images, device, seed):
-    """Resident activations U[0,1) (post-ReLU-like) and gradient records N(0,1)."""
+def synthetic_records(layers, images, device, seed):
+    """Resident inputs U[0,1) (post-ReLU-like) and gradient records N(0,1), in the
+    shapes the reference's hooks leave (curvatures.py:319-323)."""
     g = torch.Generator(device=device)
     g.manual_seed(seed)
-    recs = []
-    for d_in, d_out in dims:
-        a = torch.rand(images, d_in, device=device, generator=g)
-        gr = torch.randn(images, d_out, device=device, generator=g)
-        recs.append((a, gr))
-    return recs
+    return [(torch.rand(images, *l.in_shape, device=device, generator=g),
+             torch.randn(images, *l.out_shape, device=device, generator=g)) for l in layers]
 
 
-def cpu_baseline(dims, images, batch, budget_s=12.0):
+def cpu_baseline(layers, images, batch, budget_s=12.0):
     """The reference's CPU op sequence (oracle/cpu_ref_torch.py) on the same workload,
-    bounded to ~budget_s seconds; returns (images/s, cores, sample description)."""
+    bounded to ~budget_s seconds of whole passes; returns (images/s, cores, sample)."""
     from oracle import cpu_ref_torch as C
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     torch.set_num_threads(threads)
     rng = np.random.default_rng(0)
-    recs = [(torch.from_numpy(rng.random((images, a), dtype=np.float32)),
-             torch.from_numpy(rng.standard_normal((images, g), dtype=np.float32))) for a, g in dims]
+    recs = [(torch.from_numpy(rng.random((images, *l.in_shape), dtype=np.float32)),
+             torch.from_numpy(rng.standard_normal((images, *l.out_shape), dtype=np.float32)))
+            for l in layers]
     done, t0 = 0, time.perf_counter()
     passes = 0
     while True:
         state = {}
         for i in range(0, images, batch):
-            for li, (a, gr) in enumerate(recs):
-                C.linear_update(state, li, a[i:i + batch], gr[i:i + batch], True)
+            for li, (l, (a, gr)) in enumerate(zip(layers, recs)):
+                if l.kind == "linear":
+                    C.linear_update(state, li, a[i:i + batch], gr[i:i + batch], True)
+                else:
+                    C.conv_update(state, li, a[i:i + batch], gr[i:i + batch], l.k, l.pad, l.stride, True)
         C.invert(state, *DAMPING)
         done += images
         passes += 1
@@ -117,7 +144,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="mlp", choices=["mlp", "wide"])
+    ap.add_argument("--config", default="mlp", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=4096, help="per-rank batch")
     ap.add_argument("--images", type=int, default=60000, help="images per rank per pass")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -136,11 +163,11 @@ def main():
     from bnn_kfac_amd.curvatures import KFAC
     from bnn_kfac_amd.distributed import DistributedKFAC
 
-    dims = layer_dims(args.config)
+    specs = CONFIGS[args.config]
     net = build_model(args.config, device)
-    layers = [m for m in net.modules() if isinstance(m, torch.nn.Linear)]
+    layers = [m for m in net.modules() if isinstance(m, (torch.nn.Linear, torch.nn.Conv2d))]
     kfac = DistributedKFAC(net) if world > 1 else KFAC(net)
-    recs = synthetic_records(dims, args.images, device, seed=1234 + rank)
+    recs = synthetic_records(specs, args.images, device, seed=1234 + rank)
     starts = list(range(0, args.images, args.batch))
 
     def one_pass():
@@ -188,16 +215,16 @@ def main():
 
     # roofline of the dominant kernel: algorithmic flops of one launch (= one
     # update of one batch) / its measured duration, averaged over the timed region
-    fpi = flops_per_image(dims)
+    fpi = flops_per_image(specs)
     flops_timed = fpi * args.images * args.steps
     achieved = flops_timed / (tiles_ms * 1e-3) / 1e12 if tiles_ms > 0 else None
-    traffic = load_traffic()
+    traffic = load_traffic() if args.config == "mlp" else None  # PMC summary is of the MLP run
     roofline = {"bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": (achieved / MFMA_F32_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
                 "kernel": "kfac_factor_tiles", "launches": tiles_n,
                 "avg_launch_us": 1e3 * tiles_ms / max(tiles_n, 1),
                 "flops_per_launch": fpi * args.batch,
-                "algorithmic_bytes_per_launch": bytes_per_image(dims) * args.batch}
+                "algorithmic_bytes_per_launch": bytes_per_image(specs) * args.batch}
     breakdown = {"factor_tiles_ms_per_step": tiles_ms / args.steps,
                  "factor_reduce_ms_per_step": red_ms / args.steps,
                  "invert_ms_per_step": inv_ms / args.steps,
@@ -205,7 +232,7 @@ def main():
 
     e2e = None
     if not args.no_e2e and world == 1:
-        x = torch.rand(args.images, 784, device=device)
+        x = torch.rand(args.images, *specs[0].in_shape, device=device)
         crit = torch.nn.CrossEntropyLoss()
 
         def e2e_pass():
@@ -229,7 +256,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        v, cores, sample = cpu_baseline(dims, args.images, args.batch)
+        v, cores, sample = cpu_baseline(specs, args.images, args.batch)
         cpu = {"value": v, "unit": "images/s", "cores": cores, "kind": "port", "sample": sample}
 
     if rank == 0:
@@ -237,9 +264,8 @@ def main():
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
                "data": "synthetic (resident U[0,1) activations, N(0,1) output-gradient records)",
-               "config": {"workload": f"{args.config.upper()} {'-'.join(str(d[0]) for d in dims)}-10 KFAC factor "
-                                      f"pass over {args.images} images/rank (batch {args.batch}/rank) + "
-                                      f"invert{DAMPING}",
+               "config": {"workload": f"{NAMES[args.config]} KFAC factor pass over {args.images} "
+                                      f"images/rank (batch {args.batch}/rank) + invert{DAMPING}",
                           "global_batch": args.batch * world, "images_per_rank": args.images,
                           "parallelism": f"dp{world}"},
                "roofline": roofline, "cpu_baseline": cpu, "breakdown": breakdown,

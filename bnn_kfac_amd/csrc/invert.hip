@@ -35,6 +35,7 @@ namespace kfac {
 constexpr int NB = 64;      // fp64 tile edge
 constexpr int DP = NB + 2;  // LDS pitch (doubles): conflict-free MFMA operand reads
 constexpr int IMAXJ = 8;
+constexpr int MERGE_T = 24;  // <= this many 64-tiles per edge: merged (one-launch) steps
 
 typedef double doublex4 __attribute__((ext_vector_type(4)));
 
@@ -49,6 +50,7 @@ struct InvJobDev {
   int* info;
   double scale, shift;
   int n, T, Np, kind;
+  int xw;      // final strictly-lower X tiles in W (merged step) instead of X
 };
 
 struct InvArgs {
@@ -150,7 +152,7 @@ __device__ __forceinline__ double fast_rcp(double d) {
 // Z updates are 16x16 MFMA blocks spread over the 4 waves.  dg (>= NB+352 doubles)
 // receives the pivots; its tail is scratch.
 template <int PARTS = 7>  // ablation: bit0 elimination, bit1 panel, bit2 trailing
-__device__ void diag_factor(double* S, double* Y, double* dg) {
+__device__ __forceinline__ void diag_factor(double* S, double* Y, double* dg) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int e = tid; e < NB * NB; e += NTHREADS) Y[(e >> 6) * DP + (e & 63)] = 0.0;
   __syncthreads();
@@ -434,9 +436,112 @@ __global__ __launch_bounds__(NTHREADS) void inv_step(InvArgs args) {
   store_tile(tile_ptr(J.X, J.Np, d, d), S1, J.Np);
 }
 
-// final inverse X tile (a >= b): strictly-lower tiles live in W (see inv_step)
+// ------------------------------------------- two-launch step (large factors)
+// For many tiles per edge (T > MERGE_T) the panel is formed ONCE per step
+// (inv_panel, C in place in W and the final X[k][j] in place in X) and
+// inv_update applies it: the merged step's per-workgroup panel recomputation
+// would triple the trailing GEMM work there.  Final X stays entirely in X.
+// update k
+__global__ __launch_bounds__(NTHREADS) void inv_update(InvArgs args) {
+  __shared__ __attribute__((aligned(16))) double A[NB * DP];
+  __shared__ __attribute__((aligned(16))) double B[NB * DP];
+  __shared__ __attribute__((aligned(16))) double Y[NB * DP];
+  __shared__ double dg[NB + 352];  // pivots + elimination broadcast buffers
+  const int jb = find_job(args, blockIdx.x);
+  const InvJobDev& J = args.job[jb];
+  const int k = args.step, T = J.T;
+  const int local = blockIdx.x - args.begin[jb];
+  const int nTrail = (T - k - 1) * (T - k) / 2;
+  if (k < 0 || local < nTrail) {
+    int i = k + 1, j = k + 1;
+    if (k >= 0) {
+      int a, b;
+      tri_decode(local, a, b);
+      i = k + 1 + a;
+      j = k + 1 + b;
+    }
+    const bool factor = (i == k + 1 && j == k + 1);
+    doublex4 acc[4];
+    if (k >= 0) {
+      load_tile(A, tile_ptr(J.W, J.Np, i, k), J.Np);
+      load_tile(B, tile_ptr(J.W, J.Np, j, k), J.Np);
+      __syncthreads();
+      gemm64<true>(A, B, acc);
+    }
+    if (!factor) {
+      store_acc_global(tile_ptr(J.W, J.Np, i, j), J.Np, acc, -1.0, true);
+      return;
+    }
+    // the updated diagonal tile is consumed right here (never written back)
+    __syncthreads();
+    load_tile(A, tile_ptr(J.W, J.Np, i, i), J.Np);
+    __syncthreads();
+    if (k >= 0) {
+      const int w = threadIdx.x >> 6, col = threadIdx.x & 15;
+#pragma unroll
+      for (int b4 = 0; b4 < 4; ++b4)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) A[(16 * w + acc_row64(v)) * DP + 16 * b4 + col] -= acc[b4][v];
+      __syncthreads();
+    }
+    diag_factor(A, Y, dg);
+    if (threadIdx.x == 0 && J.info) {
+      for (int c = 0; c < NB; ++c) {
+        const int g = i * NB + c;
+        if (g < J.n && !(dg[c] > 0.0)) {
+          atomicCAS(J.info, 0, g + 1);
+          break;
+        }
+      }
+    }
+    store_tile(tile_ptr(J.X, J.Np, i, i), Y, J.Np);
+    return;
+  }
+  // Z[i][j] -= C[i][k] X[k][j]   (i > k >= j)
+  const int u = local - nTrail;
+  const int i = k + 1 + u / (k + 1), j = u % (k + 1);
+  load_tile(A, tile_ptr(J.W, J.Np, i, k), J.Np);
+  load_tile(B, tile_ptr(J.X, J.Np, k, j), J.Np);
+  __syncthreads();
+  doublex4 acc[4];
+  gemm64<false>(A, B, acc);
+  store_acc_global(tile_ptr(J.X, J.Np, i, j), J.Np, acc, -1.0, true);
+}
+
+
+// -------------------------------------------------------------------- panel k
+__global__ __launch_bounds__(NTHREADS) void inv_panel(InvArgs args) {
+  __shared__ __attribute__((aligned(16))) double A[NB * DP];
+  __shared__ __attribute__((aligned(16))) double Xk[NB * DP];
+  const int jb = find_job(args, blockIdx.x);
+  const InvJobDev& J = args.job[jb];
+  const int k = args.step, T = J.T;
+  const int local = blockIdx.x - args.begin[jb];
+  const int nC = T - k - 1;
+  load_tile(Xk, tile_ptr(J.X, J.Np, k, k), J.Np);
+  doublex4 acc[4];
+  if (local < nC) {  // C[i][k] = R'[i][k] X[k][k]^T
+    const int i = k + 1 + local;
+    double* t = tile_ptr(J.W, J.Np, i, k);
+    load_tile(A, t, J.Np);
+    __syncthreads();
+    gemm64<true>(A, Xk, acc);
+    store_acc_global(t, J.Np, acc, 1.0, false);
+  } else {           // X[k][j] = X[k][k] Z[k][j]
+    const int j = local - nC;
+    double* t = tile_ptr(J.X, J.Np, k, j);
+    load_tile(A, t, J.Np);
+    __syncthreads();
+    gemm64<false>(Xk, A, acc);
+    store_acc_global(t, J.Np, acc, 1.0, false);
+  }
+}
+
+
+// final inverse X tile (a >= b): with the merged step the strictly-lower tiles live
+// in W (see inv_step), with the two-launch step everything is in X
 __device__ __forceinline__ const double* x_tile(const InvJobDev& J, int a, int b) {
-  return tile_ptr(a > b ? J.W : J.X, J.Np, a, b);
+  return tile_ptr(a > b && J.xw ? J.W : J.X, J.Np, a, b);
 }
 
 // Y[a][b] = sum_{m >= a} X[m][a]^T X[m][b]   (lower tiles, a >= b)
@@ -481,7 +586,7 @@ __global__ __launch_bounds__(NTHREADS) void inv_out(InvArgs args) {
     double v;
     if (J.kind == KFAC_OUT_INV_CHOL) {
       const int r = n - 1 - c, q = n - 1 - i;  // L[i][c] = X[r][q], r >= q
-      v = (i >= c) ? ((r >> 6) > (q >> 6) ? J.W : J.X)[(int64_t)r * J.Np + q] : 0.0;
+      v = (i >= c) ? ((r >> 6) > (q >> 6) && J.xw ? J.W : J.X)[(int64_t)r * J.Np + q] : 0.0;
     } else {
       const int a = n - 1 - i, b = n - 1 - c;
       v = (a >= b) ? J.Tm[(int64_t)a * J.Np + b] : J.Tm[(int64_t)b * J.Np + a];
@@ -538,20 +643,38 @@ static int invert_group(const kfac_invert_job* jobs, int njobs, char* ws, int32_
     Tmax = std::max(Tmax, d.T);
     any_inverse |= jb.out_kind == KFAC_OUT_INVERSE;
   }
+  // latency-bound (few tiles per edge): one launch per step; else panel once per step
+  const bool merged = Tmax <= MERGE_T;
+  for (int i = 0; i < njobs; ++i) args.job[i].xw = merged;
   int rc;
   if (info) {
     if (hipMemsetAsync(info, 0, sizeof(int32_t) * njobs, s) != hipSuccess) return KFAC_ELAUNCH;
   }
   rc = launch(inv_build, args, [](const InvJobDev& d) { return d.T * (d.T + 1) / 2; }, s);
   if (rc) return rc;
-  for (int k = -1; k < Tmax; ++k) {
-    args.step = k;
-    rc = launch(inv_step, args, [k](const InvJobDev& d) {
-      if (k < 0) return 1;
-      if (k + 1 < d.T) return (d.T - k - 1) * (d.T - k) / 2 + (d.T - k - 1) * (k + 1);
-      return k + 1 == d.T ? k : 0;  // last row of X
-    }, s);
+  if (merged) {
+    for (int k = -1; k < Tmax; ++k) {
+      args.step = k;
+      rc = launch(inv_step, args, [k](const InvJobDev& d) {
+        if (k < 0) return 1;
+        if (k + 1 < d.T) return (d.T - k - 1) * (d.T - k) / 2 + (d.T - k - 1) * (k + 1);
+        return k + 1 == d.T ? k : 0;  // last row of X
+      }, s);
+      if (rc) return rc;
+    }
+  } else {
+    args.step = -1;
+    rc = launch(inv_update, args, [](const InvJobDev&) { return 1; }, s);
     if (rc) return rc;
+    for (int k = 0; k < Tmax; ++k) {
+      args.step = k;
+      rc = launch(inv_panel, args, [k](const InvJobDev& d) { return k < d.T ? d.T - 1 : 0; }, s);
+      if (rc) return rc;
+      rc = launch(inv_update, args, [k](const InvJobDev& d) {
+        return k + 1 < d.T ? (d.T - k - 1) * (d.T - k) / 2 + (d.T - k - 1) * (k + 1) : 0;
+      }, s);
+      if (rc) return rc;
+    }
   }
   if (any_inverse) {
     rc = launch(inv_xtx, args,
