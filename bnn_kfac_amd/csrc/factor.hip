@@ -49,7 +49,9 @@ __device__ __forceinline__ void factor_task(const FactorJobDev& J, int local, fl
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int qi = wave >> 1, qj = wave & 1;
   const bool diag = ti == tj;
-  const bool active = !(diag && qi < qj);  // strictly-upper quadrant of a diagonal tile
+  // strictly-upper quadrant of a diagonal tile, or a quadrant wholly in the tile
+  // padding (rows or columns >= n): no MFMA work (the reduce never reads it)
+  const bool active = !(diag && qi < qj) && ti * TILE + qi * 32 < J.n && tj * TILE + qj * 32 < J.n;
   floatx16 acc;
 #pragma unroll
   for (int v = 0; v < 16; ++v) acc[v] = 0.f;
@@ -147,7 +149,7 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, int loca
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int qi = wave >> 1, qj = wave & 1;
   const bool same = ti == tj;
-  const bool active = !(same && qi < qj);
+  const bool active = !(same && qi < qj) && ti * TILE + qi * 32 < J.n && tj * TILE + qj * 32 < J.n;
   floatx16 acc[NACC];
 #pragma unroll
   for (int c = 0; c < NACC; ++c)
