@@ -11,11 +11,14 @@
 //   2. kfac_factor_reduce: per tile, sum the slabs in split order, apply
 //      F = beta*F + alpha*sum, write the tile and its mirror (LDS transpose),
 //      so F stays exactly symmetric.
+#include <utility>
+#include <vector>
+
 #include "kfac_common.h"
 
 namespace kfac {
 
-constexpr int MAXJ = 8;  // factor jobs per launch (kernarg budget)
+constexpr int MAXJ = 16;  // factor jobs per launch (kernarg budget: ~3 KB of 4 KB)
 
 struct FactorJobDev {
   OpDev x;
@@ -37,6 +40,26 @@ struct FactorArgs {
   FactorJobDev job[MAXJ];
 };
 
+// Narrow factors (n <= 32): the 4 waves hold partial sums of quadrant (0,0) over
+// disjoint K subsets; sum them through LDS in wave order (deterministic) and store
+// the quadrant.  `lds` is free (the caller's stage loop has ended with a barrier).
+__device__ __forceinline__ void store_narrow(float* out, floatx16& acc, float* lds) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (wave > 0) {
+#pragma unroll
+    for (int v = 0; v < 16; ++v) lds[((wave - 1) * 16 + v) * 64 + lane] = acc[v];
+  }
+  __syncthreads();
+  if (wave != 0) return;
+#pragma unroll
+  for (int w = 0; w < 3; ++w)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[v] += lds[(w * 16 + v) * 64 + lane];
+#pragma unroll
+  for (int v = 0; v < 16; ++v) out[acc_row(v, lane) * TILE + (lane & 31)] = acc[v];
+}
+
 template <int LAYOUT>
 __device__ __forceinline__ void factor_task(const FactorJobDev& J, int local, float* lds) {
   // split-major order: consecutive tasks share the rows [k0, k1) of the operand
@@ -55,7 +78,13 @@ __device__ __forceinline__ void factor_task(const FactorJobDev& J, int local, fl
   floatx16 acc;
 #pragma unroll
   for (int v = 0; v < 16; ++v) acc[v] = 0.f;
-  contract_tile<LAYOUT, LAYOUT>(J.x, ti * TILE, J.x, tj * TILE, k0, k1, diag, active, lds, acc);
+  const bool narrow = J.n <= 32;  // one 32x32 quadrant: the 4 waves split K instead
+  contract_tile<LAYOUT, LAYOUT>(J.x, ti * TILE, J.x, tj * TILE, k0, k1, diag, active, lds, acc,
+                                narrow);
+  if (narrow) {
+    store_narrow(J.slab + ((size_t)tile * J.splits + split) * TILE * TILE, acc, lds);
+    return;
+  }
   if (!active) return;
   float* out = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE;
   const int col = qj * 32 + (lane & 31);
@@ -150,6 +179,7 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, int loca
   const int qi = wave >> 1, qj = wave & 1;
   const bool same = ti == tj;
   const bool active = !(same && qi < qj) && ti * TILE + qi * 32 < J.n && tj * TILE + qj * 32 < J.n;
+  const bool narrow = J.n <= 32;  // one 32x32 quadrant: the 4 waves split K instead
   floatx16 acc[NACC];
 #pragma unroll
   for (int c = 0; c < NACC; ++c)
@@ -179,7 +209,14 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, int loca
       if (!same) pb.fixup(kst, slot + BK * TILE);
       stage_barrier();  // stage st visible to all waves; everyone is done with st-1's slot
       if (st + NSLOT - 1 < nst) issue(st + NSLOT - 1);
-      if (active) {
+      if (narrow) {
+        const float* a = slot + h * TILE + rr;
+#pragma unroll
+        for (int s2 = 0; s2 < BK / 8; ++s2) {
+          const int ks = 2 * (wave * (BK / 8) + s2);
+          acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ks * TILE], a[ks * TILE], acc[0], 0, 0, 0);
+        }
+      } else if (active) {
         const float* a = slot + h * TILE + qi * 32 + rr;
         const float* b = slot + (same ? 0 : BK * TILE) + h * TILE + qj * 32 + rr;
         float av[BK / 2], bv[BK / 2];
@@ -193,6 +230,11 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, int loca
           acc[s2 % NACC] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s2], bv[s2], acc[s2 % NACC], 0, 0, 0);
       }
     }
+  }
+  if (narrow) {  // (narrow => one tile, diagonal: A and B panels are the same)
+    __syncthreads();
+    store_narrow(J.slab + ((size_t)tile * J.splits + split) * TILE * TILE, acc[0], lds);
+    return;
   }
   if (!active) return;
   float* out = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE;
@@ -209,7 +251,7 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, int loca
 // operand allows it, else the register-staged path for its layout.
 constexpr int FACTOR_LDS = (4 * PANEL > 2 * GSLOT) ? 4 * PANEL : 2 * GSLOT;
 
-__global__ __launch_bounds__(NTHREADS) void kfac_factor_tiles(FactorArgs args) {
+__global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles(FactorArgs args) {
   __shared__ __attribute__((aligned(16))) float lds[FACTOR_LDS];
   const int task = xcd_task(blockIdx.x, gridDim.x);
   int j = 0;
@@ -227,9 +269,18 @@ __global__ __launch_bounds__(NTHREADS) void kfac_factor_tiles(FactorArgs args) {
   }
 }
 
+// One block = one 4-row strip of one 64x64 tile.  Each float4 of the strip is
+// summed by 4 threads over interleaved splits (part p: splits p, p+4, ...); the
+// partials combine in LDS in part order (deterministic; no atomics), then
+// F = beta*F + alpha*sum and the mirrored upper element (same value: F stays
+// exactly symmetric).  16 blocks per tile keep jobs with one tile and many splits
+// (narrow conv factors: ~1000 slabs) parallel.
+constexpr int RSTRIP = 4;  // rows per reduce block
+
 __global__ __launch_bounds__(NTHREADS) void kfac_factor_reduce(FactorArgs args) {
-  __shared__ float strip[16 * LDP];
-  const int gtile = blockIdx.x >> 2, s0 = (blockIdx.x & 3) * 16;
+  __shared__ float4 part_sum[4][64];
+  __shared__ float tot[RSTRIP][TILE + 1];
+  const int gtile = blockIdx.x / (TILE / RSTRIP), s0 = (blockIdx.x % (TILE / RSTRIP)) * RSTRIP;
   int j = 0;
   while (j + 1 < args.njobs && gtile >= args.tile_end[j]) ++j;
   const FactorJobDev& J = args.job[j];
@@ -238,48 +289,56 @@ __global__ __launch_bounds__(NTHREADS) void kfac_factor_reduce(FactorArgs args) 
   tri_decode(tile, ti, tj);
   const int i0 = ti * TILE, j0 = tj * TILE, n = J.n;
   const bool diag = ti == tj;
-  const int tid = threadIdx.x, r = tid >> 4, c4 = (tid & 15) * 4;
+  const int part = threadIdx.x >> 6, f = threadIdx.x & 63;  // f: float4 of the 4 x 64 strip
+  const int r = f >> 4, c4 = (f & 15) * 4;
   const float4* slab =
       reinterpret_cast<const float4*>(J.slab + (size_t)tile * J.splits * TILE * TILE) +
       (((s0 + r) * TILE + c4) >> 2);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   const int S = J.splits;
-  int sp = 0;
-  for (; sp + 4 <= S; sp += 4) {
+  int sp = part;
+  for (; sp + 12 < S; sp += 16) {  // four splits of this part in flight
     const float4 a = slab[(size_t)(sp + 0) * (TILE * TILE / 4)];
-    const float4 b = slab[(size_t)(sp + 1) * (TILE * TILE / 4)];
-    const float4 c = slab[(size_t)(sp + 2) * (TILE * TILE / 4)];
-    const float4 d = slab[(size_t)(sp + 3) * (TILE * TILE / 4)];
+    const float4 b = slab[(size_t)(sp + 4) * (TILE * TILE / 4)];
+    const float4 c = slab[(size_t)(sp + 8) * (TILE * TILE / 4)];
+    const float4 d = slab[(size_t)(sp + 12) * (TILE * TILE / 4)];
     acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
     acc.x += b.x; acc.y += b.y; acc.z += b.z; acc.w += b.w;
     acc.x += c.x; acc.y += c.y; acc.z += c.z; acc.w += c.w;
     acc.x += d.x; acc.y += d.y; acc.z += d.z; acc.w += d.w;
   }
-  for (; sp < S; ++sp) {
+  for (; sp < S; sp += 4) {
     const float4 a = slab[(size_t)sp * (TILE * TILE / 4)];
     acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
   }
-  const float sum[4] = {acc.x, acc.y, acc.z, acc.w};
-  const int gi = i0 + s0 + r;
+  part_sum[part][f] = acc;
+  __syncthreads();
+  if (part == 0) {
+    float4 t = part_sum[0][f];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int c = c4 + q, gj = j0 + c;
-    if (gi >= n || gj >= n || (diag && c > s0 + r)) continue;
-    float* f = J.F + (int64_t)gi * J.ldF + gj;
-    const float val = J.beta == 0.f ? J.alpha * sum[q] : J.beta * (*f) + J.alpha * sum[q];
-    *f = val;
-    strip[r * LDP + c] = val;
+    for (int p = 1; p < 4; ++p) {
+      const float4 u = part_sum[p][f];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    const float sum[4] = {t.x, t.y, t.z, t.w};
+    const int gi = i0 + s0 + r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = c4 + q, gj = j0 + c;
+      float val = 0.f;
+      if (gi < n && gj < n && !(diag && c > s0 + r)) {
+        float* fp = J.F + (int64_t)gi * J.ldF + gj;
+        val = J.beta == 0.f ? J.alpha * sum[q] : J.beta * (*fp) + J.alpha * sum[q];
+        *fp = val;
+      }
+      tot[r][c] = val;
+    }
   }
   __syncthreads();
-  // mirror: F[j0 + c][i0 + s0 + rr] = strip[rr][c] (diag tiles: strictly-lower sources only)
-  const int c = tid >> 2, r4 = (tid & 3) * 4;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int rr = r4 + q;
-    const int si = i0 + s0 + rr, sj = j0 + c;  // source element
-    if (si >= n || sj >= n || (diag && c >= s0 + rr)) continue;
-    J.F[(int64_t)sj * J.ldF + si] = strip[rr * LDP + c];
-  }
+  // mirror: F[j0 + c][i0 + s0 + rr] = tot[rr][c] (diag tiles: strictly-lower sources)
+  const int c = threadIdx.x >> 2, rr = threadIdx.x & 3;
+  const int si = i0 + s0 + rr, sj = j0 + c;
+  if (si < n && sj < n && !(diag && c >= s0 + rr)) J.F[(int64_t)sj * J.ldF + si] = tot[rr][c];
 }
 
 // ------------------------------------------------------------------- host side
@@ -368,7 +427,8 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
   }
   {
     ProfScope ps(KFAC_PROF_FACTOR_REDUCE, stream);
-    hipLaunchKernelGGL(kfac_factor_reduce, dim3(tiles * 4), dim3(NTHREADS), 0, stream, args);
+    hipLaunchKernelGGL(kfac_factor_reduce, dim3(tiles * (TILE / RSTRIP)), dim3(NTHREADS), 0, stream,
+                       args);
   }
   KFAC_CHECK_LAUNCH();
   return KFAC_OK;
@@ -386,10 +446,30 @@ static size_t group_ws(const kfac_factor_job* jobs, int njobs) {
 
 using namespace kfac;
 
+// Row-major jobs share launches (up to MAXJ each): their K-steps cost alike, so the
+// planner's equal-step split balances them.  Each channel-major / im2col job gets
+// a launch (and a plan) of its own: a K-step of a gather-bound operand costs far
+// more than one of a row-major MFMA tile, and mixing them leaves the fast tasks
+// idle behind the slow ones (LeNet-5: 1.35 ms grouped vs 0.94 ms per-job).
+static void launch_groups(const kfac_factor_job* jobs, int njobs, std::vector<kfac_factor_job>& rm,
+                          std::vector<std::pair<const kfac_factor_job*, int>>& groups) {
+  rm.clear();
+  groups.clear();
+  for (int i = 0; i < njobs; ++i)
+    if (jobs[i].x.layout == KFAC_ROWMAJOR) rm.push_back(jobs[i]);
+  for (size_t g = 0; g < rm.size(); g += MAXJ)
+    groups.emplace_back(rm.data() + g, (int)std::min<size_t>(MAXJ, rm.size() - g));
+  for (int i = 0; i < njobs; ++i)
+    if (jobs[i].x.layout != KFAC_ROWMAJOR) groups.emplace_back(jobs + i, 1);
+}
+
 extern "C" size_t kfac_factor_workspace_bytes(const kfac_factor_job* jobs, int njobs) {
   if (!jobs || njobs <= 0) return 0;
+  std::vector<kfac_factor_job> rm;
+  std::vector<std::pair<const kfac_factor_job*, int>> groups;
+  launch_groups(jobs, njobs, rm, groups);
   size_t m = 0;
-  for (int g = 0; g < njobs; g += MAXJ) m = std::max(m, group_ws(jobs + g, std::min(MAXJ, njobs - g)));
+  for (const auto& g : groups) m = std::max(m, group_ws(g.first, g.second));
   return m;
 }
 
@@ -401,10 +481,13 @@ extern "C" int kfac_factor_update(const kfac_factor_job* jobs, int njobs, void* 
     if (!valid_operand(j.x) || !j.F || j.ldF < factor_n(j)) return KFAC_EINVAL;
     if ((int64_t)factor_n(j) > (int64_t)1 << 20) return KFAC_EINVAL;
   }
-  // Groups run back to back on the stream, reusing the same workspace.
-  for (int g = 0; g < njobs; g += MAXJ) {
-    const int rc = factor_group(jobs + g, std::min(MAXJ, njobs - g), (char*)workspace,
-                                workspace_bytes, (hipStream_t)stream);
+  // Launch groups run back to back on the stream, reusing the same workspace.
+  std::vector<kfac_factor_job> rm;
+  std::vector<std::pair<const kfac_factor_job*, int>> groups;
+  launch_groups(jobs, njobs, rm, groups);
+  for (const auto& g : groups) {
+    const int rc = factor_group(g.first, g.second, (char*)workspace, workspace_bytes,
+                                (hipStream_t)stream);
     if (rc != KFAC_OK) return rc;
   }
   return KFAC_OK;

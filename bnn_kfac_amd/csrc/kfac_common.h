@@ -80,7 +80,7 @@ struct Panel<KFAC_ROWMAJOR> {
   int64_t ld, kend;
   int col, c4, r0, cols, ones;
   bool vec;
-  __device__ __forceinline__ void init(const OpDev& op, int col0, int tid, int64_t k_end) {
+  __device__ __forceinline__ void init(const OpDev& op, int col0, int tid, int64_t k_end, int64_t) {
     base = op.ptr; ld = op.ld; kend = k_end; cols = op.cols; ones = op.ones;
     c4 = (tid & 15) * 4; r0 = tid >> 4; col = col0 + c4;
     vec = (col + 3 < cols) && ((ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(base) & 15) == 0);
@@ -115,24 +115,26 @@ struct Panel<KFAC_ROWMAJOR> {
   }
 };
 
+// CHANNEL and PATCH walk the K rows (image b, position l) incrementally: loads are
+// issued for k_first, k_first + BK, ... in order, so one division at init replaces
+// a 64-bit division per stage.
 template <>
 struct Panel<KFAC_CHANNEL> {
   static constexpr int PITCH = LDP;
   const float* base;
-  int64_t L, sB, kend;
+  int64_t L, sB, kend, b, l;  // (b, l) of row k + r for the next load
   int r, c0, col0, cols, ones;
-  __device__ __forceinline__ void init(const OpDev& op, int col0_, int tid, int64_t k_end) {
+  __device__ __forceinline__ void init(const OpDev& op, int col0_, int tid, int64_t k_end,
+                                       int64_t k_first) {
     base = op.ptr; L = op.L; sB = op.sB; kend = k_end; cols = op.cols; ones = op.ones;
     r = tid & 31; c0 = tid >> 5; col0 = col0_;
+    const int64_t row = k_first + r;
+    b = row / L;
+    l = row - b * L;
   }
-  __device__ __forceinline__ void load(int64_t k, float (&v)[8]) const {
-    const int64_t row = k + r;
-    const bool ok = row < kend;
-    int64_t off = 0;
-    if (ok) {
-      const int64_t b = row / L;
-      off = b * sB + (row - b * L);
-    }
+  __device__ __forceinline__ void load(int64_t k, float (&v)[8]) {
+    const bool ok = k + r < kend;
+    const int64_t off = b * sB + l;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int col = col0 + c0 + 8 * m;
@@ -140,6 +142,8 @@ struct Panel<KFAC_CHANNEL> {
       if (ok) x = col < cols ? base[off + (int64_t)col * L] : (col == ones ? 1.f : 0.f);
       v[m] = x;
     }
+    l += BK;
+    while (l >= L) { l -= L; ++b; }
   }
   __device__ __forceinline__ void store(float* lds, const float (&v)[8]) const {
 #pragma unroll
@@ -152,14 +156,20 @@ struct Panel<KFAC_PATCH> {
   static constexpr int PITCH = LDP;
   static constexpr int KZERO = -1, KONES = -2;
   const float* base;
-  int64_t L, sB, kend;
-  int r, c0, H, W, Wo, sh, sw, ph, pw;
+  int64_t sB, kend, b;  // image of row k + r for the next load
+  int r, c0, H, W, Ho, Wo, sh, sw, ph, pw, oh, ow;
   int coff[8];
   int kij[8];  // (ki << 16) | kj, or KZERO / KONES
-  __device__ __forceinline__ void init(const OpDev& op, int col0, int tid, int64_t k_end) {
-    base = op.ptr; L = op.L; sB = op.sB; kend = k_end;
-    H = op.H; W = op.W; Wo = op.Wo; sh = op.sh; sw = op.sw; ph = op.ph; pw = op.pw;
+  __device__ __forceinline__ void init(const OpDev& op, int col0, int tid, int64_t k_end,
+                                       int64_t k_first) {
+    base = op.ptr; sB = op.sB; kend = k_end;
+    H = op.H; W = op.W; Ho = op.Ho; Wo = op.Wo; sh = op.sh; sw = op.sw; ph = op.ph; pw = op.pw;
     r = tid & 31; c0 = tid >> 5;
+    const int64_t row = k_first + r;
+    b = row / op.L;
+    const int l = (int)(row - b * op.L);
+    oh = l / Wo;
+    ow = l - oh * Wo;
     const int kk = op.kh * op.kw;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
@@ -175,19 +185,10 @@ struct Panel<KFAC_PATCH> {
       }
     }
   }
-  __device__ __forceinline__ void load(int64_t k, float (&v)[8]) const {
-    const int64_t row = k + r;
-    const bool ok = row < kend;
-    int64_t off = 0;
-    int ihb = 0, iwb = 0;
-    if (ok) {
-      const int64_t b = row / L;
-      const int l = (int)(row - b * L);
-      const int oh = l / Wo, ow = l - oh * Wo;
-      ihb = oh * sh - ph;
-      iwb = ow * sw - pw;
-      off = b * sB + (int64_t)ihb * W + iwb;
-    }
+  __device__ __forceinline__ void load(int64_t k, float (&v)[8]) {
+    const bool ok = k + r < kend;
+    const int ihb = oh * sh - ph, iwb = ow * sw - pw;
+    const int64_t off = b * sB + (int64_t)ihb * W + iwb;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       float x = 0.f;
@@ -202,6 +203,11 @@ struct Panel<KFAC_PATCH> {
       }
       v[m] = x;
     }
+    ow += BK;
+    while (ow >= Wo) {
+      ow -= Wo;
+      if (++oh == Ho) { oh = 0; ++b; }
+    }
   }
   __device__ __forceinline__ void store(float* lds, const float (&v)[8]) const {
 #pragma unroll
@@ -213,19 +219,21 @@ struct Panel<KFAC_PATCH> {
 // acc(wave quadrant) += sum_{k in [k0,k1)} A[k][i0 + qi*32 + i] * B[k][j0 + qj*32 + j]
 // lds: 2 buffers x 2 panels x PANEL floats.  `same` = B panel identical to A's.
 // `active` = this wave's quadrant is needed (waves always join staging/barriers).
+// `narrow`: only quadrant (0,0) is needed (factor edge <= 32): every wave computes
+// it over its own quarter of each stage's K rows (the caller sums the 4 partials).
 template <int LA, int LB>
 __device__ __forceinline__ void contract_tile(const OpDev& opA, int i0, const OpDev& opB, int j0,
                                               int64_t k0, int64_t k1, bool same, bool active,
-                                              float* lds, floatx16& acc) {
+                                              float* lds, floatx16& acc, bool narrow = false) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int qi = wave >> 1, qj = wave & 1;
+  const int qi = narrow ? 0 : wave >> 1, qj = narrow ? 0 : wave & 1;
   const int h = lane >> 5, rr = lane & 31;
 
   Panel<LA> pa;
   Panel<LB> pb;
-  pa.init(opA, i0, tid, k1);
-  pb.init(opB, j0, tid, k1);
+  pa.init(opA, i0, tid, k1, k0);
+  pb.init(opB, j0, tid, k1, k0);
   float va[8], vb[8];
 
   // buffer c: A panel at lds + 2*c*PANEL, B panel right after it
@@ -243,9 +251,16 @@ __device__ __forceinline__ void contract_tile(const OpDev& opA, int i0, const Op
       if (!same) pb.load(k + BK, vb);
     }
     float* bcur = lds + 2 * cur * PANEL;
-    if (active) {
-      const float* a = bcur + h * Panel<LA>::PITCH + qi * 32 + rr;
-      const float* b = bcur + (same ? 0 : PANEL) + h * Panel<LB>::PITCH + qj * 32 + rr;
+    const float* a = bcur + h * Panel<LA>::PITCH + qi * 32 + rr;
+    const float* b = bcur + (same ? 0 : PANEL) + h * Panel<LB>::PITCH + qj * 32 + rr;
+    if (narrow) {
+#pragma unroll
+      for (int s = 0; s < BK / 8; ++s) {
+        const int ks = 2 * (wave * (BK / 8) + s);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ks * Panel<LA>::PITCH], b[ks * Panel<LB>::PITCH],
+                                                   acc, 0, 0, 0);
+      }
+    } else if (active) {
 #pragma unroll
       for (int s = 0; s < BK / 2; ++s)
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[2 * s * Panel<LA>::PITCH],
