@@ -186,6 +186,8 @@ struct TriArgs {
   double* e;           // n: off-diagonal of T (e[k] = T[k+1][k])
   unsigned* bar;       // arrival counter (zeroed before the launch)
   unsigned* abort;     // timeout flag (zeroed before the launch)
+  double* U;           // n x n: row k = reflector u_k (entries k+1..n-1), or null
+  double* tau;         // n: reflector scales (0: no reflection), or null
 };
 
 __device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned* abort, unsigned target) {
@@ -267,7 +269,13 @@ __global__ __launch_bounds__(NTHREADS) void eig_tridiag(TriArgs a) {
       tau = 2.0 / (u0 * u0 + sigma);
     }
     if (wg == 0 && tid == 0) a.e[k] = beta;
-    for (int j = k + 1 + tid; j < n; j += NTHREADS) uS[j] = j == k + 1 ? u0 : xk[j];
+    const bool keep_u = a.U && wg == k % G;  // reflectors kept for the eigenvector back-transform
+    if (a.U && wg == 0 && tid == 0) a.tau[k] = tau;
+    for (int j = k + 1 + tid; j < n; j += NTHREADS) {
+      const double uj = j == k + 1 ? u0 : xk[j];
+      uS[j] = uj;
+      if (keep_u) a.U[(size_t)k * n + j] = uj;
+    }
     __syncthreads();
 
     // phase A: p_i = tau * A[i][k+1:] . u, one wave per owned row
@@ -366,6 +374,146 @@ __global__ __launch_bounds__(NTHREADS) void eig_bisect(const double* d, const do
 
 using namespace kfac;
 
+// Eigenvectors of the symmetric tridiagonal (d, e) at the bisection eigenvalues w
+// (ascending) by inverse iteration (LAPACK dstein's recipe): pivoted LU of
+// T - lam I, three solves from a pseudo-random start, normalised each time.
+// Eigenvalues closer than 1e-7 ||T||_1 form a cluster, handled by one thread in
+// order: lam is nudged apart by 10 eps ||T||_1 and every iterate is
+// Gram-Schmidt-orthogonalised against the cluster's earlier vectors.  (dstein's
+// 1e-3 threshold would chain a dense spectrum into one serial cluster; in fp64
+// inverse iteration keeps vectors with gap g orthogonal to ~eps ||T|| / g, i.e.
+// 2e-9 at this threshold, far below the fp32 output's resolution.)
+// Layouts are thread-interleaved for coalescing: Z[i * n + j] = element i of
+// eigenvector j of T; scratch[a][i][t] (5 arrays, stride `st` threads).
+__global__ __launch_bounds__(NTHREADS) void eig_tri_vectors(const double* d, const double* e,
+                                                            const double* w, int n, double* Z,
+                                                            double* scratch) {
+  const int j0 = blockIdx.x * NTHREADS + threadIdx.x;
+  const int64_t st = (int64_t)gridDim.x * NTHREADS;
+  if (j0 >= n) return;
+  double onenrm = 0.0;
+  for (int i = 0; i < n; ++i)
+    onenrm = fmax(onenrm, fabs(d[i]) + (i > 0 ? fabs(e[i - 1]) : 0.0) + (i + 1 < n ? fabs(e[i]) : 0.0));
+  const double ortol = 1e-7 * onenrm, pertol = 10.0 * 2.2e-16 * fmax(onenrm, 1e-300);
+  if (j0 > 0 && w[j0] - w[j0 - 1] <= ortol) return;  // a member, not the first of its cluster
+  double* U0 = scratch + j0;
+  double* U1 = U0 + (int64_t)n * st;
+  double* U2 = U1 + (int64_t)n * st;
+  double* Lm = U2 + (int64_t)n * st;
+  double* Pv = Lm + (int64_t)n * st;
+#define S_(a, i) a[(int64_t)(i) * st]
+  double xjm = 0.0;
+  for (int j = j0; j < n && (j == j0 || w[j] - w[j - 1] <= ortol); ++j) {
+    double lam = w[j];
+    if (j > j0 && lam - xjm < pertol) lam = xjm + pertol;
+    xjm = lam;
+    // Gaussian elimination with partial pivoting of T - lam I (U: 3 diagonals)
+    double cd = d[0] - lam, cs = n > 1 ? e[0] : 0.0;
+    for (int i = 0; i + 1 < n; ++i) {
+      const double c = e[i], a1 = d[i + 1] - lam, b1 = i + 2 < n ? e[i + 1] : 0.0;
+      double u0;
+      if (fabs(c) > fabs(cd)) {
+        const double m = cd / c;
+        u0 = c; S_(U1, i) = a1; S_(U2, i) = b1; S_(Lm, i) = m; S_(Pv, i) = 1.0;
+        cd = cs - m * a1;
+        cs = -m * b1;
+      } else {
+        const double m = cd != 0.0 ? c / cd : 0.0;
+        u0 = cd; S_(U1, i) = cs; S_(U2, i) = 0.0; S_(Lm, i) = m; S_(Pv, i) = 0.0;
+        cd = a1 - m * cs;
+        cs = b1;
+      }
+      S_(U0, i) = u0 != 0.0 ? u0 : pertol;
+    }
+    S_(U0, n - 1) = cd != 0.0 ? cd : pertol;
+    double* z = Z + j;  // element i at z[i * n]
+    for (int i = 0; i < n; ++i) {  // deterministic pseudo-random start in [-1, 1)
+      unsigned h = (unsigned)i * 2654435761u ^ ((unsigned)j * 40503u + 0x9e3779b9u);
+      h ^= h >> 15; h *= 2246822519u; h ^= h >> 13;
+      z[(int64_t)i * n] = (double)(h >> 8) * (2.0 / 16777216.0) - 1.0;
+    }
+    for (int it = 0; it < 3; ++it) {
+      double zi = z[0];
+      for (int i = 0; i + 1 < n; ++i) {  // apply the row swaps and multipliers
+        double zn = z[(int64_t)(i + 1) * n];
+        if (S_(Pv, i) != 0.0) { const double t = zi; zi = zn; zn = t; }
+        z[(int64_t)i * n] = zi;
+        zi = zn - S_(Lm, i) * zi;
+      }
+      z[(int64_t)(n - 1) * n] = zi;
+      double x2 = 0.0, x1 = zi / S_(U0, n - 1);  // back substitution
+      z[(int64_t)(n - 1) * n] = x1;
+      for (int i = n - 2; i >= 0; --i) {
+        const double x = (z[(int64_t)i * n] - S_(U1, i) * x1 - S_(U2, i) * x2) / S_(U0, i);
+        z[(int64_t)i * n] = x;
+        x2 = x1;
+        x1 = x;
+      }
+      for (int jj = j0; jj < j; ++jj) {  // orthogonalise against the cluster's earlier vectors
+        const double* y = Z + jj;
+        double dot = 0.0;
+        for (int i = 0; i < n; ++i) dot += z[(int64_t)i * n] * y[(int64_t)i * n];
+        for (int i = 0; i < n; ++i) z[(int64_t)i * n] -= dot * y[(int64_t)i * n];
+      }
+      double mx = 0.0;
+      for (int i = 0; i < n; ++i) mx = fmax(mx, fabs(z[(int64_t)i * n]));
+      const double s1 = mx > 0.0 ? 1.0 / mx : 1.0;
+      double nrm = 0.0;
+      for (int i = 0; i < n; ++i) {
+        const double v = z[(int64_t)i * n] * s1;
+        nrm += v * v;
+      }
+      const double s2 = s1 / sqrt(nrm);
+      for (int i = 0; i < n; ++i) z[(int64_t)i * n] *= s2;
+    }
+  }
+#undef S_
+}
+
+// Back-transform: v_j = H_0 H_1 ... H_{n-3} z_j (T = Q^T A Q, Q = H_0 ... H_{n-3}).
+// Columns are independent, so each block carries 4 eigenvectors through all the
+// reflectors in LDS with no grid synchronisation; output fp32 evecs[i][j].
+constexpr int BT_VECS = 4;
+
+__global__ __launch_bounds__(NTHREADS) void eig_backtransform(const double* U, const double* tau,
+                                                              const double* Z, int n, float* evecs,
+                                                              int64_t ldv) {
+  extern __shared__ double vs[];  // BT_VECS x n
+  __shared__ double red[BT_VECS][NTHREADS / 64];
+  const int j0 = blockIdx.x * BT_VECS, tid = threadIdx.x;
+  const int nv = min(BT_VECS, n - j0);
+  for (int q = 0; q < BT_VECS; ++q)
+    for (int i = tid; i < n; i += NTHREADS) vs[q * n + i] = q < nv ? Z[(size_t)i * n + j0 + q] : 0.0;
+  __syncthreads();
+  for (int k = n - 3; k >= 0; --k) {
+    const double t = tau[k];
+    if (t == 0.0) continue;  // uniform
+    const double* u = U + (size_t)k * n;
+    double s[BT_VECS] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = k + 1 + tid; i < n; i += NTHREADS) {
+      const double ui = u[i];
+#pragma unroll
+      for (int q = 0; q < BT_VECS; ++q) s[q] += ui * vs[q * n + i];
+    }
+#pragma unroll
+    for (int q = 0; q < BT_VECS; ++q) {
+      for (int o = 32; o > 0; o >>= 1) s[q] += __shfl_xor(s[q], o);
+      if ((tid & 63) == 0) red[q][tid >> 6] = s[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < BT_VECS; ++q) s[q] = t * ((red[q][0] + red[q][1]) + (red[q][2] + red[q][3]));
+    for (int i = k + 1 + tid; i < n; i += NTHREADS) {
+      const double ui = u[i];
+#pragma unroll
+      for (int q = 0; q < BT_VECS; ++q) vs[q * n + i] -= s[q] * ui;
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < n; i += NTHREADS)
+    for (int q = 0; q < nv; ++q) evecs[(int64_t)i * ldv + j0 + q] = (float)vs[q * n + i];
+}
+
 // n > EIG_LDS_MAX: tridiagonalisation plan (grid, rows per workgroup, row storage)
 struct TriPlan {
   int G, R;
@@ -374,7 +522,7 @@ struct TriPlan {
 };
 constexpr size_t TRI_LDS_BUDGET = 150 * 1024;
 
-static TriPlan tri_plan(int n) {
+static TriPlan tri_plan(int n, bool vecs) {
   TriPlan p;
   p.G = std::min(256, std::max(1, (n + 7) / 8));
   p.R = (n + p.G - 1) / p.G;
@@ -384,12 +532,17 @@ static TriPlan tri_plan(int n) {
          + align_up((size_t)2 * n * sizeof(double), 256)        // x
          + 3 * align_up((size_t)n * sizeof(double), 256)        // p, d, e
          + 2 * align_up(256 * sizeof(double), 256)              // cpart, spart
-         + (p.lds_rows ? 0 : align_up((size_t)p.G * p.R * n * sizeof(double), 256));
+         + (p.lds_rows ? 0 : align_up((size_t)p.G * p.R * n * sizeof(double), 256))
+         + (vecs ? 2 * align_up((size_t)n * n * sizeof(double), 256)  // U, Z
+                       + 5 * align_up((size_t)n * cdiv(n, NTHREADS) * NTHREADS * sizeof(double), 256)
+                       + align_up((size_t)n * sizeof(double), 256)    // tau
+                 : 0);
   return p;
 }
 
-static int tridiag_eigvals(const kfac_eig_job& j, char* ws, int32_t* info, hipStream_t stream) {
-  const TriPlan pl = tri_plan(j.n);
+static int tridiag_eig(const kfac_eig_job& j, char* ws, int32_t* info, hipStream_t stream) {
+  const bool vecs = j.evecs != nullptr;
+  const TriPlan pl = tri_plan(j.n, vecs);
   if (pl.shmem > TRI_LDS_BUDGET) return KFAC_EINVAL;
   TriArgs t{};
   t.F = j.F; t.ldF = j.ldF; t.n = j.n; t.G = pl.G; t.R = pl.R;
@@ -403,6 +556,18 @@ static int tridiag_eigvals(const kfac_eig_job& j, char* ws, int32_t* info, hipSt
   t.cpart = reinterpret_cast<double*>(q); q += align_up(256 * sizeof(double), 256);
   t.spart = reinterpret_cast<double*>(q); q += align_up(256 * sizeof(double), 256);
   t.rows_g = pl.lds_rows ? nullptr : reinterpret_cast<double*>(q);
+  if (!pl.lds_rows) q += align_up((size_t)pl.G * pl.R * j.n * sizeof(double), 256);
+  double *Z = nullptr, *scratch = nullptr;
+  if (vecs) {
+    const size_t nn = align_up((size_t)j.n * j.n * sizeof(double), 256);
+    t.U = reinterpret_cast<double*>(q); q += nn;
+    Z = reinterpret_cast<double*>(q); q += nn;
+    scratch = reinterpret_cast<double*>(q);
+    q += 5 * align_up((size_t)j.n * cdiv(j.n, NTHREADS) * NTHREADS * sizeof(double), 256);
+    t.tau = reinterpret_cast<double*>(q);
+    // reflector rows start zero below their support (the back-transform reads u[k+1..])
+    if (hipMemsetAsync(t.tau, 0, (size_t)j.n * sizeof(double), stream) != hipSuccess) return KFAC_ELAUNCH;
+  }
   if (hipMemsetAsync(ws, 0, 16, stream) != hipSuccess) return KFAC_ELAUNCH;
   const void* fn = pl.lds_rows ? reinterpret_cast<const void*>(&eig_tridiag<true>)
                                : reinterpret_cast<const void*>(&eig_tridiag<false>);
@@ -416,6 +581,19 @@ static int tridiag_eigvals(const kfac_eig_job& j, char* ws, int32_t* info, hipSt
   hipLaunchKernelGGL(eig_bisect, dim3((j.n + NTHREADS - 1) / NTHREADS), dim3(NTHREADS), 0, stream,
                      t.d, t.e, j.n, j.evals, t.abort, info);
   KFAC_CHECK_LAUNCH();
+  if (vecs) {
+    hipLaunchKernelGGL(eig_tri_vectors, dim3((j.n + NTHREADS - 1) / NTHREADS), dim3(NTHREADS), 0,
+                       stream, t.d, t.e, j.evals, j.n, Z, scratch);
+    KFAC_CHECK_LAUNCH();
+    const size_t sh = (size_t)BT_VECS * j.n * sizeof(double);
+    if (sh > TRI_LDS_BUDGET) return KFAC_EINVAL;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&eig_backtransform),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh) != hipSuccess)
+      return KFAC_ELAUNCH;
+    hipLaunchKernelGGL(eig_backtransform, dim3((j.n + BT_VECS - 1) / BT_VECS), dim3(NTHREADS), sh,
+                       stream, t.U, t.tau, Z, j.n, j.evecs, j.ldv);
+    KFAC_CHECK_LAUNCH();
+  }
   return KFAC_OK;
 }
 
@@ -426,7 +604,7 @@ extern "C" size_t kfac_eig_workspace_bytes(const kfac_eig_job* jobs, int njobs) 
   int in_group = 0;
   for (int i = 0; i < njobs; ++i) {
     if (jobs[i].n > EIG_LDS_MAX) {
-      best = std::max(best, tri_plan(jobs[i].n).ws);
+      best = std::max(best, tri_plan(jobs[i].n, jobs[i].evecs != nullptr).ws);
       continue;
     }
     if (in_group == EMAXJ) { best = std::max(best, tot); tot = 0; in_group = 0; }
@@ -442,8 +620,6 @@ extern "C" int kfac_syev(const kfac_eig_job* jobs, int njobs, void* workspace, s
   for (int i = 0; i < njobs; ++i) {
     const kfac_eig_job& j = jobs[i];
     if (!j.F || !j.evals || j.n <= 0 || j.ldF < j.n || (j.evecs && j.ldv < j.n)) return KFAC_EINVAL;
-    // large factors: eigenvalues (tridiagonal route); eigenvectors not yet
-    if (j.n > EIG_LDS_MAX && j.evecs) return KFAC_EINVAL;
   }
   if (workspace_bytes < kfac_eig_workspace_bytes(jobs, njobs)) return KFAC_EWORKSPACE;
   hipStream_t st = (hipStream_t)stream;
@@ -462,7 +638,7 @@ extern "C" int kfac_syev(const kfac_eig_job* jobs, int njobs, void* workspace, s
     if (j.n > EIG_LDS_MAX) {
       int rc = flush();  // the small group owns the workspace until its launch is queued
       if (rc != KFAC_OK) return rc;
-      rc = tridiag_eigvals(j, (char*)workspace, info ? info + i : nullptr, st);
+      rc = tridiag_eig(j, (char*)workspace, info ? info + i : nullptr, st);
       if (rc != KFAC_OK) return rc;
       continue;
     }

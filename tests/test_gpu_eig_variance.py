@@ -180,9 +180,46 @@ def test_get_eigenvalues_mlp_golden(hip_device):
     np.testing.assert_allclose(ev, want, rtol=1e-5, atol=1e-6 * np.abs(want).max())
 
 
-def test_large_eigenvectors_not_supported_yet(hip_device):
-    from bnn_kfac_amd import _native as N
+@pytest.mark.parametrize("n,kind", [(129, "sym"), (300, "repeated"), (785, "spd"), (1000, "spd")])
+def test_eigvecs_large(hip_device, n, kind):
+    """n > 128: inverse iteration on the tridiagonal + Householder back-transform.
+    fp32 output: orthonormal to 1e-5, residual |F V - V diag(w)| <= 2e-5 * |w|max, and
+    the eigenvalues equal the values-only path's."""
     from bnn_kfac_amd.utilities import symeig
-    F = torch.eye(200, device=hip_device)
-    with pytest.raises(N.NativeError):
-        symeig([F], eigenvectors=True)
+    rng = np.random.default_rng(n)
+    if kind == "repeated":  # exact 3-fold clusters of multiplicity n/3 (Gram-Schmidt path)
+        Q, _ = np.linalg.qr(rng.standard_normal((n, n)))
+        F = (Q * np.repeat([1.0, 2.0, 5.0], n // 3)) @ Q.T
+    else:
+        X = rng.standard_normal((n, n))
+        F = (X + X.T) if kind == "sym" else (X @ X.T / n + 1e-3 * np.eye(n))
+    F = F.astype(np.float32)
+    (ev, V), = symeig([_t(F, hip_device)], eigenvectors=True)
+    ev, V = ev.cpu().numpy(), V.cpu().numpy().astype(np.float64)
+    scale = np.abs(ev).max()
+    np.testing.assert_allclose(ev, np.linalg.eigvalsh(F.astype(np.float64)), rtol=1e-9, atol=1e-11 * scale)
+    np.testing.assert_allclose(V.T @ V, np.eye(n), atol=1e-5)
+    np.testing.assert_allclose(F.astype(np.float64) @ V, V * ev, atol=2e-5 * scale)
+    (ev2, _), = symeig([_t(F, hip_device)])
+    np.testing.assert_array_equal(ev, ev2.cpu().numpy())
+
+
+def test_get_eigenvectors_mlp(hip_device):
+    """utilities.py:144-159 at the MLP's sizes (785 and 129 take the large path)."""
+    from bnn_kfac_amd.utilities import get_eigenvectors
+    rng = np.random.default_rng(3)
+    mods = [nn.Linear(784, 128), nn.Linear(128, 10)]
+    factors = {}
+    for m, (na, ng) in zip(mods, [(785, 128), (129, 10)]):
+        Xa = rng.random((2000, na)).astype(np.float32)
+        Xg = rng.standard_normal((2000, ng)).astype(np.float32)
+        factors[m] = [_t(Xa.T @ Xa / 2000, hip_device), _t(Xg.T @ Xg / 2000, hip_device)]
+    out = get_eigenvectors(factors)
+    for m, (A, G) in factors.items():
+        for Fd, V in zip((A, G), out[m]):
+            F = Fd.cpu().numpy().astype(np.float64)
+            S = F + F.T
+            V = V.cpu().numpy().astype(np.float64)
+            w = np.linalg.eigvalsh(S)
+            np.testing.assert_allclose(V.T @ V, np.eye(V.shape[0]), atol=1e-5)
+            np.testing.assert_allclose(S @ V, V * w, atol=2e-5 * np.abs(w).max())
