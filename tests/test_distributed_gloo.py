@@ -83,12 +83,13 @@ def _reference(scenario):
     return [ref.state["l0"][0], ref.state["l0"][1], ref.state["l1"][0], ref.state["l1"][1]]
 
 
-@pytest.mark.parametrize("scenario", ["even", "uneven", "two_passes"])
-def test_sharded_pass_matches_single_device(scenario):
+@pytest.mark.parametrize("scenario,world", [("even", 2), ("uneven", 2), ("two_passes", 2),
+                                            ("even", 4)])
+def test_sharded_pass_matches_single_device(scenario, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, scenario)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, scenario)) for r in range(world)]
     for p in procs:
         p.start()
     results = [q.get(timeout=120) for _ in procs]
