@@ -118,15 +118,26 @@ def check(rc: int, what: str):
         raise NativeError(f"{what} failed: {msg} ({rc})")
 
 
-def require_device(t: torch.Tensor, what: str):
+def require_device(t: torch.Tensor, what: str, owner=None):
+    """HIP device + fp32, or raise (no CPU fallback).  `owner` (e.g. the layer) is
+    only formatted into the message on failure: this runs on every update."""
+    if t.is_cuda and t.dtype == torch.float32:
+        return
+    where = f"{what} of {owner}" if owner is not None else what
     if not t.is_cuda:
-        raise NativeError(f"bnn_kfac_amd runs on the MI355X only: {what} is on {t.device} "
+        raise NativeError(f"bnn_kfac_amd runs on the MI355X only: {where} is on {t.device} "
                           f"(no CPU fallback; move the model/tensors to a HIP device)")
-    if t.dtype != torch.float32:
-        raise TypeError(f"{what}: expected float32 (the reference computes in fp32), got {t.dtype}")
+    raise TypeError(f"{where}: expected float32 (the reference computes in fp32), got {t.dtype}")
+
+
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
 def stream_handle(device: torch.device) -> int:
+    """hipStream_t of torch's current stream on `device` (the raw query avoids
+    building a Stream object per call)."""
+    if _raw_stream is not None:
+        return _raw_stream(device.index if device.index is not None else torch.cuda.current_device())
     return torch.cuda.current_stream(device).cuda_stream
 
 
@@ -136,8 +147,8 @@ class _Workspace:
     def __init__(self):
         self._bufs = {}
 
-    def get(self, device: torch.device, nbytes: int) -> torch.Tensor:
-        key = (device.index, stream_handle(device))
+    def get(self, device: torch.device, nbytes: int, stream: int = None) -> torch.Tensor:
+        key = (device.index, stream_handle(device) if stream is None else stream)
         buf = self._bufs.get(key)
         if buf is None or buf.numel() < nbytes:
             buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
@@ -153,10 +164,7 @@ def ptr(t) -> int:
 
 
 def as_array(ctype, items):
-    arr = (ctype * len(items))()
-    for i, it in enumerate(items):
-        arr[i] = it
-    return arr
+    return (ctype * len(items))(*items)
 
 
 # ------------------------------------------------------------------ op wrappers
@@ -166,9 +174,11 @@ def factor_update(jobs, device: torch.device):
     L = lib()
     arr = as_array(FactorJob, jobs)
     need = L.kfac_factor_workspace_bytes(arr, len(jobs))
-    ws = workspace.get(device, need)
-    check(L.kfac_factor_update(arr, len(jobs), ptr(ws), ws.numel(), stream_handle(device)),
-          "kfac_factor_update")
+    stream = stream_handle(device)
+    ws = workspace.get(device, need, stream)
+    rc = L.kfac_factor_update(arr, len(jobs), ws.data_ptr(), ws.numel(), stream)
+    if rc != KFAC_OK:
+        check(rc, "kfac_factor_update")
 
 
 def invert(jobs, device: torch.device) -> torch.Tensor:

@@ -35,6 +35,7 @@ struct FactorJobDev {
 
 struct FactorArgs {
   int njobs;
+  int stagger;  // start delay per dispatch round, in 512-cycle s_sleep(8) units
   int task_end[MAXJ];
   int tile_end[MAXJ];
   FactorJobDev job[MAXJ];
@@ -253,6 +254,10 @@ constexpr int FACTOR_LDS = (4 * PANEL > 2 * GSLOT) ? 4 * PANEL : 2 * GSLOT;
 
 __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles(FactorArgs args) {
   __shared__ __attribute__((aligned(16))) float lds[FACTOR_LDS];
+  // Workgroups of later dispatch rounds (blockIdx / 256: the ~4 sharing a CU) start a
+  // fraction of a stage later, so their DMA waits and barriers interleave instead of
+  // stalling all 16 waves of a CU together (measured +2.5% on the MLP update).
+  for (int i = 0; i < args.stagger * (int)(blockIdx.x >> 8); ++i) __builtin_amdgcn_s_sleep(8);
   const int task = xcd_task(blockIdx.x, gridDim.x);
   int j = 0;
   while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
@@ -392,6 +397,7 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
   plan_jobs(jobs, njobs, plans);
   FactorArgs args{};
   args.njobs = njobs;
+  args.stagger = 5;
   int tasks = 0, tiles = 0;
   size_t off = 0;
   for (int i = 0; i < njobs; ++i) {

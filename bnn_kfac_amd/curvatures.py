@@ -134,6 +134,7 @@ class KFAC(Curvature):
                     raise NotImplementedError
         self._packed = None      # flat fp32 device buffer holding every factor
         self._packed_views = {}  # layer -> (A view, G view)
+        self._layer_list = list(self.record)
 
     def reset(self):
         """Forget the accumulated factors (start a new data pass); device buffers are kept."""
@@ -149,16 +150,15 @@ class KFAC(Curvature):
 
     # ------------------------------------------------------------------ update
     def _layers(self):
-        for layer in self.model.modules():
-            if layer.__class__.__name__ in self.layer_types and \
-                    layer.__class__.__name__ in ['Linear', 'Conv2d']:
-                yield layer
+        """KFAC'd layers in modules() order (curvatures.py:334-337).  Only layers
+        hooked at construction have records, so the list is fixed then."""
+        return self._layer_list
 
     @staticmethod
     def _operands(layer, forward: Tensor, backward: Tensor):
         """Operand descriptors replacing curvatures.py:341-356's unfold/permute/t()."""
-        N.require_device(forward, f"input of {layer}")
-        N.require_device(backward, f"output gradient of {layer}")
+        N.require_device(forward, "input", layer)
+        N.require_device(backward, "output gradient", layer)
         has_bias = layer.bias is not None
         if layer.__class__.__name__ == 'Conv2d':
             if isinstance(layer.padding, str):
@@ -214,10 +214,13 @@ class KFAC(Curvature):
         """(A, G, beta): where this update writes and whether it accumulates."""
         if layer in self.state:
             A, G = self.state[layer]
+            own = self._packed_views.get(layer)
+            if own is not None and own[0] is A and own[1] is G:
+                return A, G, 1.0  # our own packed views: shapes/layout known
             for F_, n in ((A, nA), (G, nG)):
                 if F_.shape != (n, n):
                     raise RuntimeError(f"state of {layer} has shape {tuple(F_.shape)}, update gives {n}x{n}")
-                N.require_device(F_, f"state of {layer}")
+                N.require_device(F_, "state", layer)
                 if F_.stride(1) != 1:
                     raise RuntimeError("KFAC state factors must be row-major")
             return A, G, 1.0

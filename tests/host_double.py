@@ -30,5 +30,5 @@ def fake_factor_update(jobs, device):
 
 def install(monkeypatch):
     from bnn_kfac_amd import _native as N
-    monkeypatch.setattr(N, "require_device", lambda t, what: None)
+    monkeypatch.setattr(N, "require_device", lambda t, what, owner=None: None)
     monkeypatch.setattr(N, "factor_update", fake_factor_update)

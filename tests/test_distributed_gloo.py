@@ -29,7 +29,7 @@ def _worker(rank, world, port, result_q, scenario):
         import host_double
         from bnn_kfac_amd import _native as N
         from bnn_kfac_amd.distributed import DistributedKFAC
-        N.require_device = lambda t, what: None
+        N.require_device = lambda t, what, owner=None: None
         N.factor_update = host_double.fake_factor_update
         torch.manual_seed(0)
         net = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.ReLU(), torch.nn.Linear(5, 3))
