@@ -186,9 +186,10 @@ def invert(jobs, device: torch.device) -> torch.Tensor:
     L = lib()
     arr = as_array(InvertJob, jobs)
     need = L.kfac_invert_workspace_bytes(arr, len(jobs))
-    ws = workspace.get(device, need)
-    info = torch.zeros(len(jobs), dtype=torch.int32, device=device)
-    check(L.kfac_invert(arr, len(jobs), ptr(ws), ws.numel(), ptr(info), stream_handle(device)),
+    stream = stream_handle(device)
+    ws = workspace.get(device, need, stream)
+    info = torch.empty(len(jobs), dtype=torch.int32, device=device)  # zeroed by kfac_invert
+    check(L.kfac_invert(arr, len(jobs), ws.data_ptr(), ws.numel(), info.data_ptr(), stream),
           "kfac_invert")
     return info
 

@@ -275,7 +275,7 @@ class KFAC(Curvature):
             first, second = value
             pair = []
             for F_ in (first, second):
-                N.require_device(F_, f"state of {layer}")
+                N.require_device(F_, "state", layer)
                 out = torch.empty_like(F_, memory_format=torch.contiguous_format)
                 jobs.append(N.invert_job(F_, out, s ** 0.5, n ** 0.5))
                 pair.append(out)

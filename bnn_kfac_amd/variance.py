@@ -128,7 +128,7 @@ def regression_inverse_factors(kfac, N_data: float, tau: float) -> List[Tuple[Te
     for layer, (q, h) in kfac.state.items():
         pair = []
         for F_ in (q, h):
-            N.require_device(F_, f"state of {layer}")
+            N.require_device(F_, "state", layer)
             out = torch.empty_like(F_, memory_format=torch.contiguous_format)
             jobs.append(N.invert_job(F_, out, float(N_data), float(N_data) * float(tau), N.OUT_INVERSE))
             pair.append(out)
