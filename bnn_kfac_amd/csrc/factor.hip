@@ -104,20 +104,21 @@ __device__ __forceinline__ void factor_task(const FactorJobDev& J, int local, fl
 // ds_read_b32 halves read 32 consecutive dwords, conflict-free).  Chunks past the
 // last real column (bias ones column, tile padding) and rows past the range load
 // from a safe address and are overwritten with their fill value once landed.
-constexpr int GSLOT = 2 * BK * TILE;  // floats per ring slot (A and B panels)
-
+// GBK rows per stage; each thread owns NCH = GBK/16 of a panel's 16-byte chunks.
+template <int GBK>
 struct GldsPanel {
+  static constexpr int NCH = GBK / 16;
   const float* base;
   int64_t ld, kend;
-  int ch[2];       // this thread's two 16-byte chunks of a panel (0..511)
-  int col[2];      // first column of each chunk
-  bool real[2];    // chunk holds matrix data (else fill)
-  float4 fill[2];  // fill value of a non-real chunk (ones column -> 1)
+  int ch[NCH];       // this thread's 16-byte chunks of a panel (GBK x 16 chunks)
+  int col[NCH];      // first column of each chunk
+  bool real[NCH];    // chunk holds matrix data (else fill)
+  float4 fill[NCH];  // fill value of a non-real chunk (ones column -> 1)
   __device__ __forceinline__ void init(const OpDev& op, int col0, int w, int lane, int64_t k_end) {
     base = op.ptr; ld = op.ld; kend = k_end;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      ch[i] = (w * 2 + i) * 64 + lane;
+    for (int i = 0; i < NCH; ++i) {
+      ch[i] = (w * NCH + i) * 64 + lane;
       col[i] = col0 + (ch[i] & 15) * 4;
       real[i] = col[i] < op.cols;
       float f[4];
@@ -126,20 +127,20 @@ struct GldsPanel {
       fill[i] = make_float4(f[0], f[1], f[2], f[3]);
     }
   }
-  // issue the two LDS-DMA loads of stage rows [k, k+BK) into `slot` (panel base)
+  // issue the LDS-DMA loads of stage rows [k, k+GBK) into `slot` (panel base)
   __device__ __forceinline__ void issue(int64_t k, float* slot, int w) const {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NCH; ++i) {
       const int64_t row = k + (ch[i] >> 4);
       const int64_t r = row < kend ? row : kend - 1;
       const float* src = base + r * ld + (real[i] ? col[i] : 0);
-      __builtin_amdgcn_global_load_lds(src, slot + (w * 2 + i) * 256, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src, slot + (w * NCH + i) * 256, 16, 0, 0);
     }
   }
   // after landing: overwrite chunks that must not hold matrix data
   __device__ __forceinline__ void fixup(int64_t k, float* slot) const {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NCH; ++i) {
       const bool okrow = k + (ch[i] >> 4) < kend;
       if (!real[i] || !okrow) {
         // inline asm: the explicit vm_wait already covers this lane's DMA; a plain
@@ -154,10 +155,16 @@ struct GldsPanel {
 };
 
 __device__ __forceinline__ void vm_wait(int n) {
-  // counted waits need immediates
-  if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // counted waits need immediates: n = DMA instructions allowed to stay in flight
+  switch (n) {
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
 }
 
 __device__ __forceinline__ void stage_barrier() {
@@ -168,7 +175,7 @@ __device__ __forceinline__ void stage_barrier() {
 // NSLOT ring slots (2: one stage in flight, 4 WGs/CU; 3: two in flight, 3 WGs/CU);
 // NACC independent accumulators per wave (k-steps interleaved) to keep back-to-back
 // MFMAs off the 64-cycle dependent-accumulator latency.
-template <int NSLOT, int NACC>
+template <int GBK, int NSLOT, int NACC>
 __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, int local, float* lds) {
   const int tiles = J.t * (J.t + 1) / 2;
   const int split = local / tiles, tile = local - split * tiles;
@@ -188,46 +195,48 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, int loca
     for (int v = 0; v < 16; ++v) acc[c][v] = 0.f;
 
   if (k1 > k0) {
-    GldsPanel pa, pb;
+    constexpr int GSLOT = 2 * GBK * TILE;  // floats per ring slot (A and B panels)
+    GldsPanel<GBK> pa, pb;
     pa.init(J.x, ti * TILE, wave, lane, k1);
     pb.init(J.x, tj * TILE, wave, lane, k1);
-    const int nst = (int)((k1 - k0 + BK - 1) / BK);
-    const int per = same ? 2 : 4;  // LDS-DMA instructions per stage per thread
+    const int nst = (int)((k1 - k0 + GBK - 1) / GBK);
+    const int per = (same ? 1 : 2) * GldsPanel<GBK>::NCH;  // LDS-DMA instructions per stage per thread
     auto issue = [&](int st) {
       float* slot = lds + (st % NSLOT) * GSLOT;
-      pa.issue(k0 + (int64_t)st * BK, slot, wave);
-      if (!same) pb.issue(k0 + (int64_t)st * BK, slot + BK * TILE, wave);
+      pa.issue(k0 + (int64_t)st * GBK, slot, wave);
+      if (!same) pb.issue(k0 + (int64_t)st * GBK, slot + GBK * TILE, wave);
     };
-    issue(0);
-    if (NSLOT == 3 && nst > 1) issue(1);
+#pragma unroll
+    for (int p0 = 0; p0 < NSLOT - 1; ++p0)
+      if (p0 < nst) issue(p0);
     const int h = lane >> 5, rr = lane & 31;
     for (int st = 0; st < nst; ++st) {
-      // stage st landed (with 3 slots, st+1 may still be in flight)
-      vm_wait(NSLOT == 3 && st + 1 < nst ? per : 0);
+      // stage st landed; the stages issued after it (up to NSLOT-2) may still fly
+      vm_wait(per * min(NSLOT - 2, nst - 1 - st));
       float* slot = lds + (st % NSLOT) * GSLOT;
-      const int64_t kst = k0 + (int64_t)st * BK;
+      const int64_t kst = k0 + (int64_t)st * GBK;
       pa.fixup(kst, slot);
-      if (!same) pb.fixup(kst, slot + BK * TILE);
+      if (!same) pb.fixup(kst, slot + GBK * TILE);
       stage_barrier();  // stage st visible to all waves; everyone is done with st-1's slot
       if (st + NSLOT - 1 < nst) issue(st + NSLOT - 1);
       if (narrow) {
         const float* a = slot + h * TILE + rr;
 #pragma unroll
-        for (int s2 = 0; s2 < BK / 8; ++s2) {
-          const int ks = 2 * (wave * (BK / 8) + s2);
+        for (int s2 = 0; s2 < GBK / 8; ++s2) {
+          const int ks = 2 * (wave * (GBK / 8) + s2);
           acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ks * TILE], a[ks * TILE], acc[0], 0, 0, 0);
         }
       } else if (active) {
         const float* a = slot + h * TILE + qi * 32 + rr;
-        const float* b = slot + (same ? 0 : BK * TILE) + h * TILE + qj * 32 + rr;
-        float av[BK / 2], bv[BK / 2];
+        const float* b = slot + (same ? 0 : GBK * TILE) + h * TILE + qj * 32 + rr;
+        float av[GBK / 2], bv[GBK / 2];
 #pragma unroll
-        for (int s2 = 0; s2 < BK / 2; ++s2) {
+        for (int s2 = 0; s2 < GBK / 2; ++s2) {
           av[s2] = a[2 * s2 * TILE];
           bv[s2] = b[2 * s2 * TILE];
         }
 #pragma unroll
-        for (int s2 = 0; s2 < BK / 2; ++s2)
+        for (int s2 = 0; s2 < GBK / 2; ++s2)
           acc[s2 % NACC] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s2], bv[s2], acc[s2 % NACC], 0, 0, 0);
       }
     }
@@ -250,10 +259,10 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, int loca
 
 // One launch per grouped update: each task takes the LDS-DMA path when its job's
 // operand allows it, else the register-staged path for its layout.
-constexpr int FACTOR_LDS = (4 * PANEL > 2 * GSLOT) ? 4 * PANEL : 2 * GSLOT;
-
-__global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles(FactorArgs args) {
-  __shared__ __attribute__((aligned(16))) float lds[FACTOR_LDS];
+template <int GBK, int NSLOT>
+__global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs args) {
+  constexpr int RING = NSLOT * 2 * GBK * TILE;
+  __shared__ __attribute__((aligned(16))) float lds[(4 * PANEL > RING) ? 4 * PANEL : RING];
   // Workgroups of later dispatch rounds (blockIdx / 256: the ~4 sharing a CU) start a
   // fraction of a stage later, so their DMA waits and barriers interleave instead of
   // stalling all 16 waves of a CU together (measured +2.5% on the MLP update).
@@ -264,7 +273,7 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles(FactorArgs args
   const FactorJobDev& J = args.job[j];
   const int local = task - J.task_begin;
   if (J.glds) {
-    factor_task_glds<2, 1>(J, local, lds);
+    factor_task_glds<GBK, NSLOT, 1>(J, local, lds);
     return;
   }
   switch (J.x.layout) {
@@ -273,6 +282,9 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles(FactorArgs args
     default: factor_task<KFAC_PATCH>(J, local, lds); break;
   }
 }
+
+// production configuration: 32-row stages, 2-slot ring (one stage in flight)
+#define kfac_factor_tiles kfac_factor_tiles_t<32, 2>
 
 // One block = one 4-row strip of one 64x64 tile.  Each float4 of the strip is
 // summed by 4 threads over interleaved splits (part p: splits p, p+4, ...); the

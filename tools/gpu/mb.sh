@@ -1,2 +1,2 @@
 set -o pipefail
-cd tools/microbench && timeout -k 10 120 ./syrk_mb 1024 && timeout -k 10 120 ./syrk_mb 1280 && timeout -k 10 120 ./syrk_mb 768 && timeout -k 10 120 ./syrk_mb 1024
+cd tools/microbench && timeout -k 10 120 ./syrk_mb 1024 && timeout -k 10 120 ./syrk_mb 1024

@@ -63,11 +63,13 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 4; ++i) { la.job[i].slab = (float*)((char*)ws + o2); o2 += plans[i].slab_bytes; }
     for (int i = 0; i < 4; ++i)
       la.job[i].glds = jobs[i].x.cols % 4 == 0;
-    for (int stg : {0, 3, 4, 6}) {
-      la.stagger = stg;
-      float t0 = time_tiles(kfac_factor_tiles, la, lt, 50);
-      printf("target %5d tasks %5d chunk %4lld stagger %d | tiles %6.2f us (%5.1f TF)\n", target, lt,
-             (long long)plans[0].chunk, stg, t0, flops / t0 / 1e6);
+    la.stagger = 5;
+    struct V { const char* name; TilesK k; } vs[] = {
+        {"BK32 x2 (prod)", kfac_factor_tiles_t<32, 2>}, {"BK16 x3", kfac_factor_tiles_t<16, 3>},
+        {"BK16 x4", kfac_factor_tiles_t<16, 4>}, {"BK32 x3", kfac_factor_tiles_t<32, 3>}};
+    for (auto& v : vs) {
+      float t0 = time_tiles(v.k, la, lt, 50);
+      printf("target %5d tasks %5d | %-15s %6.2f us (%5.1f TF)\n", target, lt, v.name, t0, flops / t0 / 1e6);
     }
   }
   return 0;
