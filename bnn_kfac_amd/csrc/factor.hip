@@ -63,9 +63,8 @@ __device__ __forceinline__ void store_narrow(float* out, floatx16& acc, float* l
 
 template <int LAYOUT>
 __device__ __forceinline__ void factor_task(const FactorJobDev& J, int local, float* lds) {
-  // split-major order: consecutive tasks share the rows [k0, k1) of the operand
-  const int tiles = J.t * (J.t + 1) / 2;
-  const int split = local / tiles, tile = local - split * tiles;
+  // tile-major order: a tile's splits are consecutive tasks (one XCD; see the reduce)
+  const int tile = local / J.splits, split = local - tile * J.splits;
   int ti, tj;
   tri_decode(tile, ti, tj);
   const int64_t k0 = (int64_t)split * J.chunk;
@@ -177,8 +176,7 @@ __device__ __forceinline__ void stage_barrier() {
 // MFMAs off the 64-cycle dependent-accumulator latency.
 template <int GBK, int NSLOT, int NACC>
 __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, int local, float* lds) {
-  const int tiles = J.t * (J.t + 1) / 2;
-  const int split = local / tiles, tile = local - split * tiles;
+  const int tile = local / J.splits, split = local - tile * J.splits;
   int ti, tj;
   tri_decode(tile, ti, tj);
   const int64_t k0 = (int64_t)split * J.chunk;
@@ -297,7 +295,10 @@ constexpr int RSTRIP = 4;  // rows per reduce block
 __global__ __launch_bounds__(NTHREADS) void kfac_factor_reduce(FactorArgs args) {
   __shared__ float4 part_sum[4][64];
   __shared__ float tot[RSTRIP][TILE + 1];
-  const int gtile = blockIdx.x / (TILE / RSTRIP), s0 = (blockIdx.x % (TILE / RSTRIP)) * RSTRIP;
+  // same proportional XCD mapping as the tiles launch: a tile's strips run on the XCD
+  // whose L2 holds its freshly written slabs
+  const int rb = xcd_task(blockIdx.x, gridDim.x);
+  const int gtile = rb / (TILE / RSTRIP), s0 = (rb % (TILE / RSTRIP)) * RSTRIP;
   int j = 0;
   while (j + 1 < args.njobs && gtile >= args.tile_end[j]) ++j;
   const FactorJobDev& J = args.job[j];
