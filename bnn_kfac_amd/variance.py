@@ -88,6 +88,21 @@ def kron_quadform(terms: Sequence[Tuple[Tensor, Tensor, Tensor]], lower: bool = 
     return (out, v) if per_term else out
 
 
+def layer_jacobians(output: Tensor, layers: Sequence[torch.nn.Module], grad_outputs: Tensor) -> List[Tensor]:
+    """[J_i] for several layers from ONE backward pass: the same vectors as the
+    reference's per-parameter `gradient` calls (classification_ll_block.py:128-130,
+    sampling_free/utils.py:221-226), which each run a full backward."""
+    params = [p for layer in layers for p in layer.parameters()]
+    grads = torch.autograd.grad(output, params, grad_outputs=grad_outputs, retain_graph=True,
+                                allow_unused=True)
+    out, k = [], 0
+    for layer in layers:
+        n = len(list(layer.parameters()))
+        out.append(torch.cat([torch.flatten(g) for g in grads[k:k + n]], dim=0))
+        k += n
+    return out
+
+
 def kfac_predictive_std(kfac, output: Tensor, grad_outputs: Tensor, layers: Iterable = None,
                         per_layer: bool = False):
     """The reference's `pred_std` for one test batch (classification_ll_block.py:118-132):
@@ -95,10 +110,11 @@ def kfac_predictive_std(kfac, output: Tensor, grad_outputs: Tensor, layers: Iter
     `output` weighted by `grad_outputs` w.r.t. the layer's [W, b]."""
     if layers is None:
         layers = [m for m in list(kfac.model.modules())[1:] if m in kfac.state]
+    layers = list(layers)
     terms = []
-    for layer in layers:
+    for layer, J in zip(layers, layer_jacobians(output, layers, grad_outputs)):
         LA, LG = kfac.inv_state[layer]
-        terms.append((layer_jacobian(output, layer, grad_outputs), LA, LG))
+        terms.append((J, LA, LG))
     res = kron_quadform(terms, lower=True, abs_sum=True, per_term=per_layer)
     if per_layer:
         return float(res[0][0]), res[1][:, 0]

@@ -223,3 +223,19 @@ def test_get_eigenvectors_mlp(hip_device):
             w = np.linalg.eigvalsh(S)
             np.testing.assert_allclose(V.T @ V, np.eye(V.shape[0]), atol=1e-5)
             np.testing.assert_allclose(S @ V, V * w, atol=2e-5 * np.abs(w).max())
+
+
+def test_layer_jacobians_one_backward(hip_device):
+    """variance.layer_jacobians (one backward pass) == the reference's per-parameter
+    gradient calls (classification_ll_block.py:128-130)."""
+    from models_for_tests import BaseNet750
+    from bnn_kfac_amd.variance import argmax_grad_outputs, layer_jacobian, layer_jacobians
+    torch.manual_seed(0)
+    net = BaseNet750().to(hip_device)
+    x = torch.rand(16, 1, 28, 28, device=hip_device)
+    out = torch.softmax(net(x), dim=1)
+    go = argmax_grad_outputs(out)
+    layers = [m for m in net.modules() if isinstance(m, (nn.Linear, nn.Conv2d))]
+    for J1, layer in zip(layer_jacobians(out, layers, go), layers):
+        J0 = layer_jacobian(out, layer, go)
+        torch.testing.assert_close(J1, J0, rtol=1e-6, atol=1e-7)

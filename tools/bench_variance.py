@@ -24,7 +24,8 @@ import torch.nn as nn
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bnn_kfac_amd.curvatures import KFAC  # noqa: E402
-from bnn_kfac_amd.variance import argmax_grad_outputs, kron_quadform, layer_jacobian  # noqa: E402
+from bnn_kfac_amd.variance import (argmax_grad_outputs, kron_quadform, layer_jacobian,  # noqa: E402
+                                   layer_jacobians)
 
 
 def basenet15k():
@@ -34,9 +35,10 @@ def basenet15k():
 
 
 def pred_std_terms(net, layers, inv_state, x):
+    """One backward pass for all layers' Jacobians (variance.layer_jacobians)."""
     out = torch.softmax(net(x), dim=1)
     go = argmax_grad_outputs(out)
-    return [(layer_jacobian(out, l, go).unsqueeze(0), *inv_state[l]) for l in layers]
+    return [(J.unsqueeze(0), *inv_state[l]) for l, J in zip(layers, layer_jacobians(out, layers, go))]
 
 
 def main():
