@@ -121,6 +121,66 @@ def kfac_predictive_std(kfac, output: Tensor, grad_outputs: Tensor, layers: Iter
     return float(res[0])
 
 
+def per_sample_predictive_std(kfac, x: Tensor, layers: Iterable = None, chunk: int = 256) -> Tensor:
+    """Predictive std of every sample of `x` as the reference computes it for a test
+    batch of ONE image (classification_ll_block.py:114-135 / the noise loop 147-165):
+    p = softmax(net(x_b)), grad_outputs = one-hot(argmax p), J_l = d(go . p)/d[W_l, b_l],
+    std_b = sum_l |J_l kron(L_A, L_G) J_l^T|.
+
+    Per-sample Jacobians come from ONE vmapped gradient per chunk (torch.func), and
+    the whole chunk is contracted by a single kfac_kron_quadform launch (nb rows per
+    layer) instead of a Python loop of single-image backward passes.  Returns (N,) fp32.
+    """
+    from collections import OrderedDict
+
+    from torch.func import functional_call, grad, vmap
+    model = kfac.model
+    if layers is None:
+        layers = [m for m in list(model.modules())[1:] if m in kfac.state]
+    layers = list(layers)
+    names = {id(p): n for n, p in model.named_parameters()}
+    pnames = [[names[id(p)] for p in layer.parameters()] for layer in layers]
+    # KFAC's full backward hooks wrap outputs in an autograd.Function that functorch
+    # transforms cannot trace: suspend every module hook for this call, then restore
+    # the exact hook dictionaries
+    kinds = ("_forward_hooks", "_forward_pre_hooks", "_backward_hooks", "_backward_pre_hooks")
+    saved = [(m, [getattr(m, k) for k in kinds]) for m in model.modules()]
+    for m, _ in saved:
+        for k in kinds:
+            setattr(m, k, OrderedDict())
+    try:
+        return _per_sample_std(kfac, model, layers, pnames, x, chunk, functional_call, grad, vmap)
+    finally:
+        for m, dicts in saved:
+            for k, d in zip(kinds, dicts):
+                setattr(m, k, d)
+
+
+def _per_sample_std(kfac, model, layers, pnames, x, chunk, functional_call, grad, vmap):
+    flat = [n for group in pnames for n in group]
+    params = {n: p.detach() for n, p in model.named_parameters()}
+    buffers = {n: b for n, b in model.named_buffers()}
+
+    def score(theta, xb):
+        full = dict(params)
+        full.update(theta)
+        p = torch.softmax(functional_call(model, (full, buffers), (xb.unsqueeze(0),)), dim=1)[0]
+        go = (p == p.max()).to(p.dtype)  # one-hot argmax (a comparison: no gradient through it)
+        return (go.detach() * p).sum()
+
+    jac = vmap(grad(score), in_dims=(None, 0))
+    out = []
+    for c0 in range(0, x.shape[0], chunk):
+        g = jac({n: params[n] for n in flat}, x[c0:c0 + chunk])
+        terms = []
+        for layer, group in zip(layers, pnames):
+            J = torch.cat([g[n].reshape(g[n].shape[0], -1) for n in group], dim=1)
+            LA, LG = kfac.inv_state[layer]
+            terms.append((J, LA, LG))
+        out.append(kron_quadform(terms, lower=True, abs_sum=True))
+    return torch.cat(out)
+
+
 def argmax_grad_outputs(pred_mean: Tensor) -> Tensor:
     """grad_outputs[:, idx] = 1 with idx = argmax per row, set for EVERY row
     (classification_ll_block.py:119-121 semantics)."""

@@ -239,3 +239,34 @@ def test_layer_jacobians_one_backward(hip_device):
     for J1, layer in zip(layer_jacobians(out, layers, go), layers):
         J0 = layer_jacobian(out, layer, go)
         torch.testing.assert_close(J1, J0, rtol=1e-6, atol=1e-7)
+
+
+def test_per_sample_predictive_std_matches_single_image_loop(hip_device):
+    """variance.per_sample_predictive_std (vmapped Jacobians, one quadform launch per
+    chunk) == the reference's loop over test batches of ONE image
+    (classification_ll_block.py:147-165)."""
+    from models_for_tests import BaseNet750
+    from bnn_kfac_amd.curvatures import KFAC
+    from bnn_kfac_amd.variance import (argmax_grad_outputs, kron_quadform, layer_jacobian,
+                                       per_sample_predictive_std)
+    torch.manual_seed(0)
+    net = BaseNet750().to(hip_device)
+    kfac = KFAC(net)
+    for _ in range(3):
+        xb = torch.rand(64, 1, 28, 28, device=hip_device)
+        logits = net(xb)
+        y = torch.distributions.Categorical(logits=logits).sample()
+        net.zero_grad()
+        torch.nn.functional.cross_entropy(logits, y).backward()
+        kfac.update(64)
+    kfac.invert(0.04, 200)
+    x = torch.rand(37, 1, 28, 28, device=hip_device)
+    got = per_sample_predictive_std(kfac, x, chunk=16).cpu().numpy()
+    layers = [m for m in list(net.modules())[1:] if m in kfac.state]
+    want = []
+    for b in range(x.shape[0]):
+        p = torch.softmax(net(x[b:b + 1]), dim=1)
+        go = argmax_grad_outputs(p)
+        terms = [(layer_jacobian(p, l, go), *kfac.inv_state[l]) for l in layers]
+        want.append(float(kron_quadform(terms)))
+    np.testing.assert_allclose(got, np.array(want), rtol=1e-5)

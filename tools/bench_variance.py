@@ -25,7 +25,7 @@ import torch.nn as nn
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bnn_kfac_amd.curvatures import KFAC  # noqa: E402
 from bnn_kfac_amd.variance import (argmax_grad_outputs, kron_quadform, layer_jacobian,  # noqa: E402
-                                   layer_jacobians)
+                                   layer_jacobians, per_sample_predictive_std)
 
 
 def basenet15k():
@@ -84,6 +84,15 @@ def main():
     torch.cuda.synchronize()
     gpu_q = (time.perf_counter() - t0) / reps
 
+    # per-sample std (the reference's noise loop: test batches of ONE image), vmapped
+    xs = torch.rand(2048, 1, 28, 28, device=dev, generator=g)
+    per_sample_predictive_std(kfac, xs[:256])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    per_sample_predictive_std(kfac, xs)
+    torch.cuda.synchronize()
+    gpu_ps_us = (time.perf_counter() - t0) / xs.shape[0] * 1e6
+
     # the reference's op sequence on the host, same weights, factors and inputs
     torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1))
     net_c = basenet15k()
@@ -108,12 +117,24 @@ def main():
         ref_vals.append(s)
     cpu_ref = (time.perf_counter() - t0) / ncpu
     cpu_q = tq / ncpu
+    # one image per "batch" on the host (the noise loop), a few images
+    t0 = time.perf_counter()
+    nimg = 8
+    for b in range(nimg):
+        out1 = torch.softmax(net_c(xs[b:b + 1].cpu()), dim=1)
+        go1 = argmax_grad_outputs(out1)
+        s1 = 0.0
+        for l in layers_c:
+            J = layer_jacobian(out1, l, go1).unsqueeze(0).detach()
+            s1 += torch.abs(J @ torch.kron(*inv_c[l]) @ J.t()).item()
+    cpu_ps_us = (time.perf_counter() - t0) / nimg * 1e6
     got = np.array([float(v) for v in vals[:ncpu]])
     rel = float(np.max(np.abs(got - np.array(ref_vals)) / np.abs(np.array(ref_vals))))
     print(json.dumps({
         "workload": f"BaseNet_15k predictive std, {nbatch} test batches of {batch}",
         "gpu_e2e_ms_per_batch": gpu_e2e * 1e3, "gpu_quadform_ms_per_batch": gpu_q * 1e3,
         "cpu_ref_ms_per_batch": cpu_ref * 1e3, "cpu_ref_kron_quadform_ms_per_batch": cpu_q * 1e3,
+        "gpu_per_sample_us": gpu_ps_us, "cpu_ref_per_sample_us": cpu_ps_us,
         "cpu_threads": torch.get_num_threads(), "cpu_batches": ncpu,
         "max_rel_diff_vs_cpu_ref": rel}))
 
