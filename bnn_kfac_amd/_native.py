@@ -34,7 +34,8 @@ class Operand(ctypes.Structure):
 
 
 class FactorJob(ctypes.Structure):
-    _fields_ = [("x", Operand), ("alpha", c_f32), ("beta", c_f32), ("F", c_vp), ("ldF", c_i64)]
+    _fields_ = [("x", Operand), ("alpha", c_f32), ("beta", c_f32), ("F", c_vp), ("ldF", c_i64),
+                ("acc", c_vp), ("acc_splits", c_i32), ("acc_beta", c_f32)]
 
 
 class InvertJob(ctypes.Structure):
@@ -58,6 +59,9 @@ SIGNATURES = {
     "kfac_factor_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(FactorJob), ctypes.c_int]),
     "kfac_factor_update": (ctypes.c_int, [ctypes.POINTER(FactorJob), ctypes.c_int, c_vp,
                                           ctypes.c_size_t, c_vp]),
+    "kfac_factor_accum_plan": (ctypes.c_int, [ctypes.POINTER(FactorJob), ctypes.c_int,
+                                              ctypes.POINTER(c_i32), ctypes.POINTER(ctypes.c_size_t)]),
+    "kfac_factor_flush": (ctypes.c_int, [ctypes.POINTER(FactorJob), ctypes.c_int, c_vp]),
     "kfac_syrk_linear": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, ctypes.c_int, c_f32, c_f32,
                                         c_vp, c_i64, c_vp, ctypes.c_size_t, c_vp]),
     "kfac_syrk_conv": (ctypes.c_int, [c_vp, c_i64] + [ctypes.c_int] * 10 + [c_f32, c_f32, c_vp,
@@ -179,6 +183,21 @@ def factor_update(jobs, device: torch.device):
     rc = L.kfac_factor_update(arr, len(jobs), ws.data_ptr(), ws.numel(), stream)
     if rc != KFAC_OK:
         check(rc, "kfac_factor_update")
+
+
+def factor_accum_plan(jobs):
+    """[(splits, bytes)] of each job's deferred-reduction accumulator."""
+    arr = as_array(FactorJob, jobs)
+    splits = (c_i32 * len(jobs))()
+    nbytes = (ctypes.c_size_t * len(jobs))()
+    check(lib().kfac_factor_accum_plan(arr, len(jobs), splits, nbytes), "kfac_factor_accum_plan")
+    return list(zip(splits, nbytes))
+
+
+def factor_flush(jobs, device: torch.device):
+    if jobs:
+        check(lib().kfac_factor_flush(as_array(FactorJob, jobs), len(jobs), stream_handle(device)),
+              "kfac_factor_flush")
 
 
 def invert(jobs, device: torch.device) -> torch.Tensor:

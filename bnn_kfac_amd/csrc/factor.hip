@@ -31,6 +31,8 @@ struct FactorJobDev {
   int task_begin;    // first global task of this job
   int glds;          // row-major, 16-byte-aligned rows: LDS-DMA kernel
   int tile_begin;    // first global tile of this job (reduce launch)
+  int accum;         // deferred reduction: `slab` is the caller's accumulator
+  float sbeta;       // accumulator update: slab = sbeta*slab + alpha*partial
 };
 
 struct FactorArgs {
@@ -41,10 +43,33 @@ struct FactorArgs {
   FactorJobDev job[MAXJ];
 };
 
+// Epilogue write of one lane's 16 partial-tile values (`at(v)` = address of value
+// v): a plain slab store, or, for a deferred-reduction job, the accumulator update
+// slab = sbeta*slab + alpha*partial (old values loaded together first).
+template <class At>
+__device__ __forceinline__ void put_partial(const FactorJobDev& J, const floatx16& acc, At at) {
+  if (!J.accum) {
+#pragma unroll
+    for (int v = 0; v < 16; ++v) *at(v) = acc[v];
+    return;
+  }
+  if (J.sbeta == 0.f) {
+#pragma unroll
+    for (int v = 0; v < 16; ++v) *at(v) = J.alpha * acc[v];
+    return;
+  }
+  float old[16];
+#pragma unroll
+  for (int v = 0; v < 16; ++v) old[v] = *at(v);
+#pragma unroll
+  for (int v = 0; v < 16; ++v) *at(v) = fmaf(J.sbeta, old[v], J.alpha * acc[v]);
+}
+
 // Narrow factors (n <= 32): the 4 waves hold partial sums of quadrant (0,0) over
 // disjoint K subsets; sum them through LDS in wave order (deterministic) and store
 // the quadrant.  `lds` is free (the caller's stage loop has ended with a barrier).
-__device__ __forceinline__ void store_narrow(float* out, floatx16& acc, float* lds) {
+__device__ __forceinline__ void store_narrow(const FactorJobDev& J, float* out, floatx16& acc,
+                                             float* lds) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   __syncthreads();
   if (wave > 0) {
@@ -57,8 +82,7 @@ __device__ __forceinline__ void store_narrow(float* out, floatx16& acc, float* l
   for (int w = 0; w < 3; ++w)
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[v] += lds[(w * 16 + v) * 64 + lane];
-#pragma unroll
-  for (int v = 0; v < 16; ++v) out[acc_row(v, lane) * TILE + (lane & 31)] = acc[v];
+  put_partial(J, acc, [&](int v) { return &out[acc_row(v, lane) * TILE + (lane & 31)]; });
 }
 
 template <int LAYOUT>
@@ -82,14 +106,12 @@ __device__ __forceinline__ void factor_task(const FactorJobDev& J, int local, fl
   contract_tile<LAYOUT, LAYOUT>(J.x, ti * TILE, J.x, tj * TILE, k0, k1, diag, active, lds, acc,
                                 narrow);
   if (narrow) {
-    store_narrow(J.slab + ((size_t)tile * J.splits + split) * TILE * TILE, acc, lds);
+    store_narrow(J, J.slab + ((size_t)tile * J.splits + split) * TILE * TILE, acc, lds);
     return;
   }
   if (!active) return;
-  float* out = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE;
-  const int col = qj * 32 + (lane & 31);
-#pragma unroll
-  for (int v = 0; v < 16; ++v) out[(qi * 32 + acc_row(v, lane)) * TILE + col] = acc[v];
+  float* out = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE + qi * 32 * TILE + qj * 32;
+  put_partial(J, acc, [&](int v) { return &out[acc_row(v, lane) * TILE + (lane & 31)]; });
 }
 
 
@@ -174,8 +196,9 @@ __device__ __forceinline__ void stage_barrier() {
 // NSLOT ring slots (2: one stage in flight, 4 WGs/CU; 3: two in flight, 3 WGs/CU);
 // NACC independent accumulators per wave (k-steps interleaved) to keep back-to-back
 // MFMAs off the 64-cycle dependent-accumulator latency.
-template <int GBK, int NSLOT, int NACC>
+template <int GBK, int NSLOT, int NACC, int MODE = 0, int SUB = 1>
 __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, int local, float* lds) {
+  static_assert(NSLOT >= 2 * SUB, "ring must hold the computed step and the next one");
   const int tile = local / J.splits, split = local - tile * J.splits;
   int ti, tj;
   tri_decode(tile, ti, tj);
@@ -192,86 +215,126 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, int loca
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[c][v] = 0.f;
 
-  if (k1 > k0) {
+  if (k1 > k0 && !(MODE & 64)) {
+    // ring of NSLOT slots of GBK rows; one barrier per step of SUB slots, so
+    // NSLOT - SUB slots are in flight while a step computes
     constexpr int GSLOT = 2 * GBK * TILE;  // floats per ring slot (A and B panels)
     GldsPanel<GBK> pa, pb;
     pa.init(J.x, ti * TILE, wave, lane, k1);
     pb.init(J.x, tj * TILE, wave, lane, k1);
-    const int nst = (int)((k1 - k0 + GBK - 1) / GBK);
-    const int per = (same ? 1 : 2) * GldsPanel<GBK>::NCH;  // LDS-DMA instructions per stage per thread
-    auto issue = [&](int st) {
-      float* slot = lds + (st % NSLOT) * GSLOT;
-      pa.issue(k0 + (int64_t)st * GBK, slot, wave);
-      if (!same) pb.issue(k0 + (int64_t)st * GBK, slot + GBK * TILE, wave);
+    const int ns = (int)((k1 - k0 + GBK - 1) / GBK);  // slots of this task
+    const int nstep = (ns + SUB - 1) / SUB;
+    const int per = (same ? 1 : 2) * GldsPanel<GBK>::NCH;  // LDS-DMA instructions per slot per thread
+    auto issue = [&](int sl) {
+      if (MODE & 4) return;
+      float* slot = lds + (sl % NSLOT) * GSLOT;
+      pa.issue(k0 + (int64_t)sl * GBK, slot, wave);
+      if (!same) pb.issue(k0 + (int64_t)sl * GBK, slot + GBK * TILE, wave);
     };
 #pragma unroll
-    for (int p0 = 0; p0 < NSLOT - 1; ++p0)
-      if (p0 < nst) issue(p0);
+    for (int p0 = 0; p0 < NSLOT - SUB; ++p0)
+      if (p0 < ns) issue(p0);
     const int h = lane >> 5, rr = lane & 31;
-    for (int st = 0; st < nst; ++st) {
-      // stage st landed; the stages issued after it (up to NSLOT-2) may still fly
-      vm_wait(per * min(NSLOT - 2, nst - 1 - st));
-      float* slot = lds + (st % NSLOT) * GSLOT;
-      const int64_t kst = k0 + (int64_t)st * GBK;
-      pa.fixup(kst, slot);
-      if (!same) pb.fixup(kst, slot + GBK * TILE);
-      stage_barrier();  // stage st visible to all waves; everyone is done with st-1's slot
-      if (st + NSLOT - 1 < nst) issue(st + NSLOT - 1);
-      if (narrow) {
-        const float* a = slot + h * TILE + rr;
+    for (int st = 0; st < nstep; ++st) {
+      // slots of step st landed; those issued after them may still fly
+      const int need = min(ns - 1, SUB * st + SUB - 1);
+      const int issued = min(ns - 1, SUB * st + NSLOT - SUB - 1);
+      vm_wait(per * (issued - need));
 #pragma unroll
-        for (int s2 = 0; s2 < GBK / 8; ++s2) {
-          const int ks = 2 * (wave * (GBK / 8) + s2);
-          acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ks * TILE], a[ks * TILE], acc[0], 0, 0, 0);
+      for (int u = 0; u < SUB; ++u) {
+        const int sl = SUB * st + u;
+        if (sl < ns) {
+          float* slot = lds + (sl % NSLOT) * GSLOT;
+          const int64_t kst = k0 + (int64_t)sl * GBK;
+          pa.fixup(kst, slot);
+          if (!same) pb.fixup(kst, slot + GBK * TILE);
         }
-      } else if (active) {
-        const float* a = slot + h * TILE + qi * 32 + rr;
-        const float* b = slot + (same ? 0 : GBK * TILE) + h * TILE + qj * 32 + rr;
-        float av[GBK / 2], bv[GBK / 2];
+      }
+      stage_barrier();  // step st visible to all waves; everyone is done with step st-1's slots
 #pragma unroll
-        for (int s2 = 0; s2 < GBK / 2; ++s2) {
-          av[s2] = a[2 * s2 * TILE];
-          bv[s2] = b[2 * s2 * TILE];
+      for (int u = 0; u < SUB; ++u) {
+        const int sl = SUB * st + NSLOT - SUB + u;
+        if (sl < ns) issue(sl);
+      }
+#pragma unroll
+      for (int u = 0; u < SUB; ++u) {
+        const int sl = SUB * st + u;
+        if (SUB > 1 && sl >= ns) break;
+        const float* slot = lds + (sl % NSLOT) * GSLOT;
+        if (narrow) {
+          const float* a = slot + h * TILE + rr;
+#pragma unroll
+          for (int s2 = 0; s2 < GBK / 8; ++s2) {
+            const int ks = 2 * (wave * (GBK / 8) + s2);
+            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ks * TILE], a[ks * TILE], acc[0], 0, 0, 0);
+          }
+        } else if (active) {
+          const float* a = slot + h * TILE + qi * 32 + rr;
+          const float* b = slot + (same ? 0 : GBK * TILE) + h * TILE + qj * 32 + rr;
+          float av[GBK / 2], bv[GBK / 2];
+#pragma unroll
+          for (int s2 = 0; s2 < GBK / 2; ++s2) {
+            if (MODE & 16) {
+              av[s2] = (float)(lane + s2);
+              bv[s2] = (float)(lane - s2);
+            } else {
+              av[s2] = a[2 * s2 * TILE];
+              bv[s2] = b[2 * s2 * TILE];
+            }
+          }
+          if (MODE & 1) __builtin_amdgcn_s_setprio(1);
+          if (MODE & 8) {
+#pragma unroll
+            for (int s2 = 0; s2 < GBK / 2; ++s2) acc[0][s2 & 15] += av[s2] * bv[s2];
+          } else {
+#pragma unroll
+            for (int s2 = 0; s2 < GBK / 2; ++s2)
+              acc[s2 % NACC] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s2], bv[s2], acc[s2 % NACC], 0, 0, 0);
+          }
+          if (MODE & 2) {
+#pragma unroll
+            for (int s2 = 0; s2 < GBK / 2; ++s2) {
+              __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // 2 DS reads
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+            }
+          }
+          if (MODE & 1) __builtin_amdgcn_s_setprio(0);
         }
-#pragma unroll
-        for (int s2 = 0; s2 < GBK / 2; ++s2)
-          acc[s2 % NACC] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s2], bv[s2], acc[s2 % NACC], 0, 0, 0);
       }
     }
   }
   if (narrow) {  // (narrow => one tile, diagonal: A and B panels are the same)
     __syncthreads();
-    store_narrow(J.slab + ((size_t)tile * J.splits + split) * TILE * TILE, acc[0], lds);
+    store_narrow(J, J.slab + ((size_t)tile * J.splits + split) * TILE * TILE, acc[0], lds);
     return;
   }
   if (!active) return;
-  float* out = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE;
-  const int col = qj * 32 + (lane & 31);
+  float* out = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE + qi * 32 * TILE + qj * 32;
 #pragma unroll
   for (int c = 1; c < NACC; ++c)
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[0][v] += acc[c][v];
-#pragma unroll
-  for (int v = 0; v < 16; ++v) out[(qi * 32 + acc_row(v, lane)) * TILE + col] = acc[0][v];
+  put_partial(J, acc[0], [&](int v) { return &out[acc_row(v, lane) * TILE + (lane & 31)]; });
 }
 
 // One launch per grouped update: each task takes the LDS-DMA path when its job's
 // operand allows it, else the register-staged path for its layout.
-template <int GBK, int NSLOT>
+template <int GBK, int NSLOT, int MODE = 0, int SUB = 1>
 __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs args) {
   constexpr int RING = NSLOT * 2 * GBK * TILE;
   __shared__ __attribute__((aligned(16))) float lds[(4 * PANEL > RING) ? 4 * PANEL : RING];
   // Workgroups of later dispatch rounds (blockIdx / 256: the ~4 sharing a CU) start a
   // fraction of a stage later, so their DMA waits and barriers interleave instead of
   // stalling all 16 waves of a CU together (measured +2.5% on the MLP update).
-  for (int i = 0; i < args.stagger * (int)(blockIdx.x >> 8); ++i) __builtin_amdgcn_s_sleep(8);
+  if (!(MODE & 32))
+    for (int i = 0; i < args.stagger * (int)(blockIdx.x >> 8); ++i) __builtin_amdgcn_s_sleep(8);
   const int task = xcd_task(blockIdx.x, gridDim.x);
   int j = 0;
   while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
   const FactorJobDev& J = args.job[j];
   const int local = task - J.task_begin;
   if (J.glds) {
-    factor_task_glds<GBK, NSLOT, 1>(J, local, lds);
+    factor_task_glds<GBK, NSLOT, 1, MODE, SUB>(J, local, lds);
     return;
   }
   switch (J.x.layout) {
@@ -281,8 +344,9 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
   }
 }
 
-// production configuration: 32-row stages, 2-slot ring (one stage in flight)
-#define kfac_factor_tiles kfac_factor_tiles_t<32, 2>
+// production configuration: 32-row stages, 2-slot ring (one stage in flight),
+// DS reads interleaved with the MFMAs (MODE 2: -1.2 us of 42 on the MLP update)
+#define kfac_factor_tiles kfac_factor_tiles_t<32, 2, 2>
 
 // One block = one 4-row strip of one 64x64 tile.  Each float4 of the strip is
 // summed by 4 threads over interleaved splits (part p: splits p, p+4, ...); the
@@ -369,7 +433,10 @@ struct Plan {
 static int factor_n(const kfac_factor_job& j) { return j.x.cols + (j.x.has_ones ? 1 : 0); }
 
 // Split K so that the whole grouped launch has ~4 tasks per CU (256 CUs) but
-// every task still runs >= 256 rows of MFMA work.
+// every task still runs >= 256 rows of MFMA work.  A job with a deferred-reduction
+// accumulator keeps the accumulator's split count (its layout): its K range is cut
+// into that many equal chunks (trailing splits of a smaller batch may be empty and
+// then contribute zero).
 static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
                       int64_t target_tasks = 1024) {
   int64_t work = 0;
@@ -383,11 +450,22 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
     Plan& p = plans[i];
     p.tiles = t * (t + 1) / 2;
     const int64_t steps = std::max<int64_t>(1, cdiv(jobs[i].x.rows, BK));
+    if (jobs[i].acc) {
+      p.splits = jobs[i].acc_splits;
+      p.chunk = cdiv(steps, (int64_t)p.splits) * BK;
+      p.slab_bytes = 0;  // partials go to the caller's accumulator
+      continue;
+    }
     const int64_t cs = std::min(chunk_steps, steps);
     p.chunk = cs * BK;
     p.splits = (int)cdiv(steps, cs);
     p.slab_bytes = align_up((size_t)p.tiles * p.splits * TILE * TILE * sizeof(float), 256);
   }
+}
+
+static size_t accum_bytes(int n, int splits) {
+  const int64_t t = cdiv(n, TILE);
+  return align_up((size_t)(t * (t + 1) / 2) * splits * TILE * TILE * sizeof(float), 256);
 }
 
 static bool valid_operand(const kfac_operand& o) {
@@ -404,38 +482,59 @@ static bool valid_operand(const kfac_operand& o) {
   }
 }
 
+static void fill_dev(FactorJobDev& d, const kfac_factor_job& jb) {
+  d.x = to_dev(jb.x);
+  d.alpha = jb.alpha;
+  d.beta = jb.beta;
+  d.F = jb.F;
+  d.ldF = jb.ldF;
+  d.n = factor_n(jb);
+  d.t = (int)cdiv(d.n, TILE);
+  d.accum = jb.acc != nullptr;
+  d.sbeta = jb.acc_beta;
+}
+
+// One reduce launch over `njobs` jobs whose slabs are described by d.slab/d.splits.
+static void launch_reduce(FactorArgs& r, int tiles, hipStream_t stream) {
+  if (tiles == 0) return;
+  ProfScope ps(KFAC_PROF_FACTOR_REDUCE, stream);
+  hipLaunchKernelGGL(kfac_factor_reduce, dim3(tiles * (TILE / RSTRIP)), dim3(NTHREADS), 0, stream,
+                     r);
+}
+
 static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t ws_bytes,
                         hipStream_t stream) {
   Plan plans[MAXJ];
   plan_jobs(jobs, njobs, plans);
   FactorArgs args{};
+  FactorArgs red{};  // the reduce launch: jobs reduced now (no accumulator)
   args.njobs = njobs;
   args.stagger = 5;
-  int tasks = 0, tiles = 0;
+  int tasks = 0, rtiles = 0;
   size_t off = 0;
   for (int i = 0; i < njobs; ++i) {
     const kfac_factor_job& jb = jobs[i];
     FactorJobDev& d = args.job[i];
-    d.x = to_dev(jb.x);
-    d.alpha = jb.alpha;
-    d.beta = jb.beta;
-    d.F = jb.F;
-    d.ldF = jb.ldF;
-    d.n = factor_n(jb);
-    d.t = (int)cdiv(d.n, TILE);
+    fill_dev(d, jb);
     d.glds = jb.x.layout == KFAC_ROWMAJOR && jb.x.rows > 0 && jb.x.cols >= 4 &&
              (jb.x.cols % 4) == 0 && (jb.x.ld % 4) == 0 &&
              (reinterpret_cast<uintptr_t>(jb.x.ptr) % 16) == 0;
     d.splits = plans[i].splits;
     d.chunk = plans[i].chunk;
-    d.slab = reinterpret_cast<float*>(ws + off);
-    off += plans[i].slab_bytes;
+    if (jb.acc) {
+      d.slab = jb.acc;
+    } else {
+      d.slab = reinterpret_cast<float*>(ws + off);
+      off += plans[i].slab_bytes;
+      FactorJobDev& e = red.job[red.njobs];
+      e = d;
+      e.tile_begin = rtiles;
+      rtiles += plans[i].tiles;
+      red.tile_end[red.njobs++] = rtiles;
+    }
     d.task_begin = tasks;
-    d.tile_begin = tiles;
     tasks += plans[i].tiles * plans[i].splits;
-    tiles += plans[i].tiles;
     args.task_end[i] = tasks;
-    args.tile_end[i] = tiles;
   }
   if (off > ws_bytes) return KFAC_EWORKSPACE;
   if (tasks == 0) return KFAC_OK;
@@ -444,11 +543,7 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
     hipLaunchKernelGGL(kfac_factor_tiles, dim3(tasks), dim3(NTHREADS), 0, stream, args);
     KFAC_CHECK_LAUNCH();
   }
-  {
-    ProfScope ps(KFAC_PROF_FACTOR_REDUCE, stream);
-    hipLaunchKernelGGL(kfac_factor_reduce, dim3(tiles * (TILE / RSTRIP)), dim3(NTHREADS), 0, stream,
-                       args);
-  }
+  launch_reduce(red, rtiles, stream);
   KFAC_CHECK_LAUNCH();
   return KFAC_OK;
 }
@@ -470,44 +565,107 @@ using namespace kfac;
 // a launch (and a plan) of its own: a K-step of a gather-bound operand costs far
 // more than one of a row-major MFMA tile, and mixing them leaves the fast tasks
 // idle behind the slow ones (LeNet-5: 1.35 ms grouped vs 0.94 ms per-job).
-static void launch_groups(const kfac_factor_job* jobs, int njobs, std::vector<kfac_factor_job>& rm,
-                          std::vector<std::pair<const kfac_factor_job*, int>>& groups) {
-  rm.clear();
+// `order` receives the caller's job index of each entry of `sorted`.
+static void launch_groups(const kfac_factor_job* jobs, int njobs, std::vector<kfac_factor_job>& sorted,
+                          std::vector<int>& order, std::vector<std::pair<int, int>>& groups) {
+  sorted.clear();
+  order.clear();
   groups.clear();
   for (int i = 0; i < njobs; ++i)
-    if (jobs[i].x.layout == KFAC_ROWMAJOR) rm.push_back(jobs[i]);
-  for (size_t g = 0; g < rm.size(); g += MAXJ)
-    groups.emplace_back(rm.data() + g, (int)std::min<size_t>(MAXJ, rm.size() - g));
+    if (jobs[i].x.layout == KFAC_ROWMAJOR) {
+      sorted.push_back(jobs[i]);
+      order.push_back(i);
+    }
+  const int nrm = (int)sorted.size();
+  for (int g = 0; g < nrm; g += MAXJ) groups.emplace_back(g, std::min(MAXJ, nrm - g));
   for (int i = 0; i < njobs; ++i)
-    if (jobs[i].x.layout != KFAC_ROWMAJOR) groups.emplace_back(jobs + i, 1);
+    if (jobs[i].x.layout != KFAC_ROWMAJOR) {
+      groups.emplace_back((int)sorted.size(), 1);
+      sorted.push_back(jobs[i]);
+      order.push_back(i);
+    }
 }
 
 extern "C" size_t kfac_factor_workspace_bytes(const kfac_factor_job* jobs, int njobs) {
   if (!jobs || njobs <= 0) return 0;
-  std::vector<kfac_factor_job> rm;
-  std::vector<std::pair<const kfac_factor_job*, int>> groups;
-  launch_groups(jobs, njobs, rm, groups);
+  std::vector<kfac_factor_job> sorted;
+  std::vector<int> order;
+  std::vector<std::pair<int, int>> groups;
+  launch_groups(jobs, njobs, sorted, order, groups);
   size_t m = 0;
-  for (const auto& g : groups) m = std::max(m, group_ws(g.first, g.second));
+  for (const auto& g : groups) m = std::max(m, group_ws(sorted.data() + g.first, g.second));
   return m;
 }
 
-extern "C" int kfac_factor_update(const kfac_factor_job* jobs, int njobs, void* workspace,
-                                  size_t workspace_bytes, kfac_stream_t stream) {
+static int validate(const kfac_factor_job* jobs, int njobs) {
   if (njobs < 0 || (njobs > 0 && !jobs)) return KFAC_EINVAL;
   for (int i = 0; i < njobs; ++i) {
     const kfac_factor_job& j = jobs[i];
     if (!valid_operand(j.x) || !j.F || j.ldF < factor_n(j)) return KFAC_EINVAL;
     if ((int64_t)factor_n(j) > (int64_t)1 << 20) return KFAC_EINVAL;
+    if (j.acc && (j.acc_splits <= 0 || j.acc_splits > (1 << 20))) return KFAC_EINVAL;
   }
-  // Launch groups run back to back on the stream, reusing the same workspace.
-  std::vector<kfac_factor_job> rm;
-  std::vector<std::pair<const kfac_factor_job*, int>> groups;
-  launch_groups(jobs, njobs, rm, groups);
+  return KFAC_OK;
+}
+
+extern "C" int kfac_factor_accum_plan(const kfac_factor_job* jobs, int njobs, int32_t* splits,
+                                      size_t* bytes) {
+  if (validate(jobs, njobs) != KFAC_OK || (njobs > 0 && (!splits || !bytes))) return KFAC_EINVAL;
+  std::vector<kfac_factor_job> sorted;
+  std::vector<int> order;
+  std::vector<std::pair<int, int>> groups;
+  launch_groups(jobs, njobs, sorted, order, groups);
+  for (auto& j : sorted) j.acc = nullptr;  // plan as an immediate update of this batch
   for (const auto& g : groups) {
-    const int rc = factor_group(g.first, g.second, (char*)workspace, workspace_bytes,
-                                (hipStream_t)stream);
+    Plan plans[MAXJ];
+    plan_jobs(sorted.data() + g.first, g.second, plans);
+    for (int k = 0; k < g.second; ++k) {
+      const int i = order[g.first + k];
+      splits[i] = plans[k].splits;
+      bytes[i] = accum_bytes(factor_n(jobs[i]), plans[k].splits);
+    }
+  }
+  return KFAC_OK;
+}
+
+extern "C" int kfac_factor_update(const kfac_factor_job* jobs, int njobs, void* workspace,
+                                  size_t workspace_bytes, kfac_stream_t stream) {
+  const int rc0 = validate(jobs, njobs);
+  if (rc0 != KFAC_OK) return rc0;
+  // Launch groups run back to back on the stream, reusing the same workspace.
+  std::vector<kfac_factor_job> sorted;
+  std::vector<int> order;
+  std::vector<std::pair<int, int>> groups;
+  launch_groups(jobs, njobs, sorted, order, groups);
+  for (const auto& g : groups) {
+    const int rc = factor_group(sorted.data() + g.first, g.second, (char*)workspace,
+                                workspace_bytes, (hipStream_t)stream);
     if (rc != KFAC_OK) return rc;
+  }
+  return KFAC_OK;
+}
+
+extern "C" int kfac_factor_flush(const kfac_factor_job* jobs, int njobs, kfac_stream_t stream) {
+  const int rc0 = validate(jobs, njobs);
+  if (rc0 != KFAC_OK) return rc0;
+  FactorArgs red{};
+  int tiles = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const kfac_factor_job& jb = jobs[i];
+    if (!jb.acc) return KFAC_EINVAL;
+    FactorJobDev& e = red.job[red.njobs];
+    fill_dev(e, jb);
+    e.slab = jb.acc;
+    e.splits = jb.acc_splits;
+    e.tile_begin = tiles;
+    tiles += e.t * (e.t + 1) / 2;
+    red.tile_end[red.njobs++] = tiles;
+    if (red.njobs == MAXJ || i == njobs - 1) {
+      launch_reduce(red, tiles, (hipStream_t)stream);
+      KFAC_CHECK_LAUNCH();
+      red = FactorArgs{};
+      tiles = 0;
+    }
   }
   return KFAC_OK;
 }

@@ -56,6 +56,22 @@ class Curvature(ABC):
         self.state = dict()
         self.inv_state = dict()
 
+    # `state` reads and writes first complete any reduction an implementation
+    # deferred (KFAC keeps a data pass's split-K partials on the device and reduces
+    # them into the factors once; see KFAC.flush).
+    @property
+    def state(self):
+        self.flush()
+        return self._state
+
+    @state.setter
+    def state(self, value):
+        self.flush()
+        self._state = value
+
+    def flush(self):
+        """Complete deferred work so that `state` holds every update so far."""
+
     @staticmethod
     def _replace(sample: Tensor, weight: Tensor, bias: Tensor = None):
         """Add a sampled offset to a layer's parameters, bias = last column
@@ -135,11 +151,26 @@ class KFAC(Curvature):
         self._packed = None      # flat fp32 device buffer holding every factor
         self._packed_views = {}  # layer -> (A view, G view)
         self._layer_list = list(self.record)
+        # Deferred reduction (kfac_factor_flush): updates keep each factor's split-K
+        # partial tiles in device accumulators; the reduce into `state` runs once,
+        # when the state is next read (invert / save / `state` / all-reduce).
+        self.defer_reduce = True
+        self._acc_buf = None     # grow-only device buffer of the accumulators
+        self._acc_flush = None   # flush jobs of the pending cycle (None: nothing pending)
+        self._acc_device = None
 
     def reset(self):
         """Forget the accumulated factors (start a new data pass); device buffers are kept."""
-        self.state = dict()
+        self._acc_flush = None
+        self._state = dict()
         self.inv_state = dict()
+
+    def flush(self):
+        """Reduce the pending accumulators into the factors (one launch; async)."""
+        jobs = getattr(self, "_acc_flush", None)
+        if jobs:
+            self._acc_flush = None
+            N.factor_flush(jobs, self._acc_device)
 
     # curvatures.py:319-323
     def _save_input(self, module, input):
@@ -212,8 +243,8 @@ class KFAC(Curvature):
 
     def _target(self, layer, nA, nG, device):
         """(A, G, beta): where this update writes and whether it accumulates."""
-        if layer in self.state:
-            A, G = self.state[layer]
+        if layer in self._state:
+            A, G = self._state[layer]
             own = self._packed_views.get(layer)
             if own is not None and own[0] is A and own[1] is G:
                 return A, G, 1.0  # our own packed views: shapes/layout known
@@ -225,7 +256,7 @@ class KFAC(Curvature):
                     raise RuntimeError("KFAC state factors must be row-major")
             return A, G, 1.0
         A, G = self._packed_views[layer]
-        self.state[layer] = [A, G]
+        self._state[layer] = [A, G]
         return A, G, 0.0
 
     def update(self, batch_size: int):
@@ -241,14 +272,46 @@ class KFAC(Curvature):
         if not prepared:
             return
         device = prepared[0][5][0].device
-        if any(layer not in self.state for layer, *_ in prepared):
+        if any(layer not in self._state for layer, *_ in prepared):
             self._ensure_packed([(p[0], p[3], p[4]) for p in prepared], device)
         jobs = []
         for layer, opA, opG, nA, nG, _keep in prepared:
             A, G, beta = self._target(layer, nA, nG, device)
             jobs.append(N.factor_job(opA, A, self._alpha(opA), beta))
             jobs.append(N.factor_job(opG, G, self._alpha(opG), beta))
+        if self.defer_reduce:
+            self._defer(jobs, device)
         N.factor_update(jobs, device)
+
+    def _defer(self, jobs, device):
+        """Point each job at its accumulator: continue the pending cycle when it
+        targets the same factors, else (first update, or new targets) flush and plan
+        a new cycle for this batch shape."""
+        pending = self._acc_flush
+        if pending is not None and (device != self._acc_device or len(pending) != len(jobs)
+                                    or any(p.F != j.F for p, j in zip(pending, jobs))):
+            self.flush()
+            pending = None
+        if pending is not None:
+            for p, j in zip(pending, jobs):
+                j.acc, j.acc_splits, j.acc_beta = p.acc, p.acc_splits, 1.0
+            return
+        plan = N.factor_accum_plan(jobs)
+        offs, total = [], 0
+        for _splits, nbytes in plan:
+            offs.append(total)
+            total += (nbytes + 255) // 256 * 256
+        buf = self._acc_buf
+        if buf is None or buf.device != device or buf.numel() < total:
+            buf = self._acc_buf = torch.empty(total, dtype=torch.uint8, device=device)
+        base = buf.data_ptr()
+        flush = []
+        for j, (splits, _nbytes), off in zip(jobs, plan, offs):
+            j.acc, j.acc_splits, j.acc_beta = base + off, splits, 0.0
+            f = N.FactorJob.from_buffer_copy(j)
+            f.alpha = 1.0  # partials already carry alpha; f.beta: 0 fresh factor, 1 existing
+            flush.append(f)
+        self._acc_flush, self._acc_device = flush, device
 
     # ------------------------------------------------------------------ invert
     def _damping(self, add, multiply):

@@ -50,20 +50,22 @@ class DistributedKFAC(KFAC):
             self._scale = float(self.world)
         else:
             self._scale = float(global_batch_size) / float(batch_size)
-        # accumulate into the rank-local state, then restore the reduced one
-        reduced = self.state
-        self.state = self._local_state
+        # accumulate into the rank-local state, then restore the reduced one (raw
+        # dicts: reading `state` would complete the deferred reduction every update)
+        reduced = self._state
+        self._state = self._local_state
         try:
             super().update(batch_size)
         finally:
-            self._local_state = self.state
-            self.state = reduced
+            self._local_state = self._state
+            self._state = reduced
         self._pending = True
 
     def allreduce(self):
         """Sum the rank-local factors over ranks and add them to `state` (one collective)."""
         if not self._pending:
             return
+        self.flush()  # the rank-local factors are complete only after the deferred reduce
         local = self._local_state
         packed = self._packed
         views_packed = packed is not None and all(
@@ -75,20 +77,20 @@ class DistributedKFAC(KFAC):
                 for A, G in local.values():
                     dist.all_reduce(A, group=self.group)
                     dist.all_reduce(G, group=self.group)
-        if not self.state:
+        if not self._state:
             # first pass: the reduced local buffer becomes the state (no copy); the next
             # local accumulation gets a fresh buffer
-            self.state = {layer: list(v) for layer, v in local.items()}
+            self._state = {layer: list(v) for layer, v in local.items()}
             self._global_buf, self._global_views = packed, self._packed_views
             self._packed = None
             self._packed_views = {}
         else:
             for layer, (A, G) in local.items():
-                if layer in self.state:
-                    self.state[layer][0] += A
-                    self.state[layer][1] += G
+                if layer in self._state:
+                    self._state[layer][0] += A
+                    self._state[layer][1] += G
                 else:
-                    self.state[layer] = [A.clone(), G.clone()]
+                    self._state[layer] = [A.clone(), G.clone()]
         self._local_state = {}
         self._pending = False
 

@@ -71,6 +71,17 @@ typedef struct kfac_factor_job {
   float beta;  /* 0 = first update assigns, 1 = later updates add (curvatures.py:359-363) */
   float* F;
   int64_t ldF;
+  /* Optional deferred reduction (NULL = reduce into F in this call).  With `acc`
+   * set, kfac_factor_update leaves F alone and keeps this factor's split-K partial
+   * tiles in the caller's accumulator instead:  acc = acc_beta*acc + alpha*partial
+   * (acc_beta 0 on the first update after a flush, 1 after).  kfac_factor_flush
+   * then writes F = beta*F + alpha*sum(acc) once, e.g. at the end of a data pass,
+   * so a pass of U updates runs U MFMA launches + 1 reduce instead of U + U.
+   * acc_splits and the size come from kfac_factor_accum_plan; F = sum of the
+   * partials either way (floating-point summation order differs).            */
+  float* acc;
+  int32_t acc_splits;
+  float acc_beta;
 } kfac_factor_job;
 
 /* Workspace (split-K slabs) needed by kfac_factor_update for these jobs. */
@@ -79,6 +90,15 @@ KFAC_API size_t kfac_factor_workspace_bytes(const kfac_factor_job* jobs, int njo
  * Replaces KFAC.update, models/curvatures.py:325-365. */
 KFAC_API int kfac_factor_update(const kfac_factor_job* jobs, int njobs, void* workspace,
                        size_t workspace_bytes, kfac_stream_t stream);
+
+/* Accumulator layout for these jobs (acc ignored): splits[j] and bytes[j] of job
+ * j's deferred-reduction accumulator, planned for this batch shape (later
+ * batches of any row count may use it).                                    */
+KFAC_API int kfac_factor_accum_plan(const kfac_factor_job* jobs, int njobs, int32_t* splits,
+                           size_t* bytes);
+/* F = beta*F + alpha*sum(acc) for every job (all must carry acc): the reduce
+ * step of kfac_factor_update, deferred (x is only read for the factor size). */
+KFAC_API int kfac_factor_flush(const kfac_factor_job* jobs, int njobs, kfac_stream_t stream);
 
 /* Single-factor conveniences (same kernels). */
 KFAC_API int kfac_syrk_linear(const float* x, int64_t B, int64_t d, int64_t ldx, int has_ones,

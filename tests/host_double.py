@@ -13,6 +13,8 @@ def _view(ptr, count):
 
 
 def fake_factor_update(jobs, device):
+    """kfac_factor_update: F = beta F + alpha X~^T X~, or with a deferred-reduction
+    accumulator (modelled as one n x n split) acc = acc_beta acc + alpha X~^T X~."""
     from bnn_kfac_amd import _native as N
     for j in jobs:
         op = j.x
@@ -21,8 +23,36 @@ def fake_factor_update(jobs, device):
         if op.has_ones:
             X = np.concatenate([X, np.ones((op.rows, 1))], axis=1)
         n = op.cols + op.has_ones
+        if j.acc:
+            assert j.acc_splits == 1
+            A = _view(j.acc, n * n).reshape(n, n)
+            new = j.alpha * (X.T @ X)
+            if j.acc_beta != 0.0:
+                new = new + j.acc_beta * A.astype(np.float64)
+            A[:] = new.astype(np.float32)
+            continue
         F = _view(j.F, n * j.ldF).reshape(n, j.ldF)
         new = j.alpha * (X.T @ X)
+        if j.beta != 0.0:
+            new = new + j.beta * F[:, :n].astype(np.float64)
+        F[:, :n] = new.astype(np.float32)
+
+
+def fake_accum_plan(jobs):
+    return [(1, (j.x.cols + j.x.has_ones) ** 2 * 4) for j in jobs]
+
+
+FLUSHES = []
+
+
+def fake_factor_flush(jobs, device):
+    """kfac_factor_flush: F = beta F + alpha acc."""
+    FLUSHES.append(len(jobs))
+    for j in jobs:
+        n = j.x.cols + j.x.has_ones
+        A = _view(j.acc, n * n).reshape(n, n).astype(np.float64)
+        F = _view(j.F, n * j.ldF).reshape(n, j.ldF)
+        new = j.alpha * A
         if j.beta != 0.0:
             new = new + j.beta * F[:, :n].astype(np.float64)
         F[:, :n] = new.astype(np.float32)
@@ -32,3 +62,5 @@ def install(monkeypatch):
     from bnn_kfac_amd import _native as N
     monkeypatch.setattr(N, "require_device", lambda t, what, owner=None: None)
     monkeypatch.setattr(N, "factor_update", fake_factor_update)
+    monkeypatch.setattr(N, "factor_accum_plan", fake_accum_plan)
+    monkeypatch.setattr(N, "factor_flush", fake_factor_flush)

@@ -105,6 +105,44 @@ def test_update_host_logic_with_double(monkeypatch):
     assert kfac.state == {} and kfac._packed is not None
 
 
+def test_deferred_reduce_host_logic(monkeypatch):
+    """Deferred reduction: a pass of updates keeps partials in accumulators and
+    reduces ONCE when `state` is read; an update after that read starts a new cycle
+    that adds to the factors (flush beta 1); results equal the immediate path."""
+    from bnn_kfac_amd.curvatures import KFAC
+    host_double.install(monkeypatch)
+    host_double.FLUSHES.clear()
+    rng = np.random.default_rng(3)
+    batches = []
+    for B in (8, 8, 5, 8):
+        batches.append([rng.random((B, 6), dtype=np.float32), rng.standard_normal((B, 5)).astype(np.float32),
+                        rng.random((B, 5), dtype=np.float32), rng.standard_normal((B, 3)).astype(np.float32)])
+
+    def run(defer, read_after):
+        net = mlp()
+        kfac = KFAC(net)
+        kfac.defer_reduce = defer
+        for i, (a1, g1, a2, g2) in enumerate(batches):
+            kfac.record[net[0]] = [torch.from_numpy(a1), torch.from_numpy(g1)]
+            kfac.record[net[2]] = [torch.from_numpy(a2), torch.from_numpy(g2)]
+            kfac.update(a1.shape[0])
+            if i == read_after:
+                _ = kfac.state  # completes the pending reduction
+        return [t.clone().numpy() for pair in kfac.state.values() for t in pair]
+
+    want = run(False, -1)
+    assert host_double.FLUSHES == []
+    got = run(True, -1)
+    assert host_double.FLUSHES == [4]  # one flush (4 factors) for 4 updates
+    for g, w in zip(got, want):
+        np.testing.assert_allclose(g, w, rtol=1e-6)
+    host_double.FLUSHES.clear()
+    got = run(True, 1)
+    assert host_double.FLUSHES == [4, 4]  # read mid-pass, then the rest of the pass
+    for g, w in zip(got, want):
+        np.testing.assert_allclose(g, w, rtol=1e-6)
+
+
 def test_save_load_roundtrip(tmp_path):
     from bnn_kfac_amd.curvatures import KFAC
     net = mlp()

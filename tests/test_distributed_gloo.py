@@ -31,6 +31,8 @@ def _worker(rank, world, port, result_q, scenario):
         from bnn_kfac_amd.distributed import DistributedKFAC
         N.require_device = lambda t, what, owner=None: None
         N.factor_update = host_double.fake_factor_update
+        N.factor_accum_plan = host_double.fake_accum_plan
+        N.factor_flush = host_double.fake_factor_flush
         torch.manual_seed(0)
         net = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.ReLU(), torch.nn.Linear(5, 3))
         kfac = DistributedKFAC(net)

@@ -193,3 +193,67 @@ def test_empty_batch_rows(hip_device):
     F = torch.zeros(6, 6, device=hip_device)
     N.factor_update([N.factor_job(N.rowmajor_operand(x, True), F, 1.0, 1.0)], hip_device)
     assert torch.equal(F, torch.zeros_like(F))
+
+
+def test_deferred_reduce_raw_abi(hip_device):
+    """kfac_factor_update with accumulators + kfac_factor_flush: F0 + sum of three
+    batches (the last one much smaller than the planned one, so trailing splits are
+    empty), exact on small integers; F stays untouched until the flush."""
+    from bnn_kfac_amd import _native as N
+    rng = np.random.default_rng(5)
+    F0 = rng.integers(-4, 5, size=(130, 130)).astype(np.float32)
+    F0 = F0 + F0.T
+    F = _t(F0, hip_device)
+    xs = [rng.integers(-3, 4, size=(B, 129)).astype(np.float32) for B in (3000, 3000, 70)]
+    xd = [_t(x, hip_device) for x in xs]
+    jobs = [N.factor_job(N.rowmajor_operand(xd[0], True), F, 1.0, 1.0)]
+    (splits, nbytes), = N.factor_accum_plan(jobs)
+    assert splits >= 2
+    acc = torch.empty(nbytes, dtype=torch.uint8, device=hip_device)
+    for i, x in enumerate(xd):
+        j = N.factor_job(N.rowmajor_operand(x, True), F, 1.0, 1.0)
+        j.acc, j.acc_splits, j.acc_beta = acc.data_ptr(), splits, 0.0 if i == 0 else 1.0
+        N.factor_update([j], hip_device)
+    np.testing.assert_array_equal(F.cpu().numpy(), F0)
+    f = N.factor_job(N.rowmajor_operand(xd[0], True), F, 1.0, 1.0)
+    f.acc, f.acc_splits = acc.data_ptr(), splits
+    N.factor_flush([f], hip_device)
+    want = F0.astype(np.float64)
+    for x in xs:
+        xo = np.concatenate([x, np.ones((x.shape[0], 1), np.float32)], 1).astype(np.float64)
+        want += xo.T @ xo
+    np.testing.assert_array_equal(F.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("model", ["mlp", "lenet"])
+def test_deferred_reduce_matches_immediate(hip_device, model):
+    """KFAC.update with the deferred reduction (default) equals the per-update
+    reduce, for row-major and conv factors, across a mid-pass `state` read."""
+    from bnn_kfac_amd.curvatures import KFAC
+    torch.manual_seed(0)
+    if model == "mlp":
+        net = nn.Sequential(nn.Linear(784, 128), nn.ReLU(), nn.Linear(128, 10)).to(hip_device)
+        shape = (784,)
+    else:
+        net = nn.Sequential(nn.Conv2d(1, 6, 5), nn.ReLU(), nn.MaxPool2d(2), nn.Conv2d(6, 16, 5),
+                            nn.ReLU(), nn.MaxPool2d(2), nn.Flatten(), nn.Linear(256, 10)).to(hip_device)
+        shape = (1, 28, 28)
+    g = torch.Generator(device=hip_device).manual_seed(1)
+    xs = [torch.rand(B, *shape, device=hip_device, generator=g) for B in (1024, 1024, 300, 1024)]
+    outs = []
+    for defer, read_at in ((False, -1), (True, -1), (True, 1)):
+        kfac = KFAC(net)
+        kfac.defer_reduce = defer
+        for i, x in enumerate(xs):
+            out = net(x)
+            net.zero_grad()
+            nn.functional.cross_entropy(out, out.argmax(1)).backward()
+            kfac.update(x.shape[0])
+            if i == read_at:
+                _ = kfac.state
+        outs.append([t.cpu().numpy() for pair in kfac.state.values() for t in pair])
+        for h in kfac.hooks:
+            h.remove()
+    for other in outs[1:]:
+        for got, want in zip(other, outs[0]):
+            np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-6 * np.abs(want).max())

@@ -65,8 +65,11 @@ int main(int argc, char** argv) {
       la.job[i].glds = jobs[i].x.cols % 4 == 0;
     la.stagger = 5;
     struct V { const char* name; TilesK k; } vs[] = {
-        {"BK32 x2 (prod)", kfac_factor_tiles_t<32, 2>}, {"BK16 x3", kfac_factor_tiles_t<16, 3>},
-        {"BK16 x4", kfac_factor_tiles_t<16, 4>}, {"BK32 x3", kfac_factor_tiles_t<32, 3>}};
+        {"prod (BK32 x2 sched)", kfac_factor_tiles}, {"no sched", kfac_factor_tiles_t<32, 2, 0>},
+        {"setprio", kfac_factor_tiles_t<32, 2, 1>}, {"no stagger", kfac_factor_tiles_t<32, 2, 2 + 32>},
+        {"16x5 sub2", kfac_factor_tiles_t<16, 5, 2, 2>}, {"32x3", kfac_factor_tiles_t<32, 3, 2>},
+        {"no DMA", kfac_factor_tiles_t<32, 2, 2 + 4>}, {"no MFMA", kfac_factor_tiles_t<32, 2, 8>},
+        {"no DMA, no LDS reads", kfac_factor_tiles_t<32, 2, 4 + 16>}};
     for (auto& v : vs) {
       float t0 = time_tiles(v.k, la, lt, 50);
       printf("target %5d tasks %5d | %-15s %6.2f us (%5.1f TF)\n", target, lt, v.name, t0, flops / t0 / 1e6);
