@@ -82,6 +82,29 @@ __device__ __forceinline__ void load_tile(double* lds, const double* g, int Np) 
   for (int q = 0; q < PER; ++q) lds[(r0 + 4 * q) * DP + c] = v[q];
 }
 
+// Up to three tiles with every load in flight together (one memory round trip
+// instead of one per tile); null destinations are skipped.
+__device__ __forceinline__ void load_tiles(double* l0, const double* g0, double* l1, const double* g1,
+                                           double* l2, const double* g2, int Np) {
+  constexpr int PER = NB * NB / NTHREADS;
+  const int c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+  double v0[PER], v1[PER], v2[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int64_t off = (int64_t)(r0 + 4 * q) * Np + c;
+    v0[q] = g0[off];
+    if (l1) v1[q] = g1[off];
+    if (l2) v2[q] = g2[off];
+  }
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int o = (r0 + 4 * q) * DP + c;
+    l0[o] = v0[q];
+    if (l1) l1[o] = v1[q];
+    if (l2) l2[o] = v2[q];
+  }
+}
+
 __device__ __forceinline__ void store_tile(double* g, const double* lds, int Np) {
   for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
     const int r = e >> 6, c = e & 63;
@@ -339,27 +362,25 @@ __device__ __forceinline__ bool step_trailing(const InvJobDev& J, int k, int loc
   int a, b;
   tri_decode(local, a, b);
   const int i = k + 1 + a, j = k + 1 + b;
-  load_tile(S0, tile_ptr(J.X, J.Np, k, k), J.Np);
-  load_tile(S1, tile_ptr(J.W, J.Np, i, k), J.Np);
-  if (j != i) load_tile(S2, tile_ptr(J.W, J.Np, j, k), J.Np);
+  const bool diag = i == k + 1 && j == k + 1;
+  // the (k+1,k+1) workgroup also prefetches its diagonal tile into the idle S2
+  load_tiles(S0, tile_ptr(J.X, J.Np, k, k), S1, tile_ptr(J.W, J.Np, i, k),
+             (j != i || diag) ? S2 : nullptr, tile_ptr(J.W, J.Np, j != i ? j : i, j != i ? k : i), J.Np);
   __syncthreads();
   panel_tile_lds(S1, S0);              // C_i
   if (j != i) panel_tile_lds(S2, S0);  // C_j
   doublex4 acc[4];
   gemm64<true>(S1, j != i ? S2 : S1, acc);
-  if (!(i == k + 1 && j == k + 1)) {
+  if (!diag) {
     store_acc_global(tile_ptr(J.W, J.Np, i, j), J.Np, acc, -1.0, true);
     return false;
   }
   // the updated diagonal tile is consumed right here (never written back)
-  __syncthreads();
-  load_tile(S0, tile_ptr(J.W, J.Np, i, i), J.Np);
-  __syncthreads();
   const int w = threadIdx.x >> 6, col = threadIdx.x & 15;
 #pragma unroll
   for (int b4 = 0; b4 < 4; ++b4)
 #pragma unroll
-    for (int v = 0; v < 4; ++v) S0[(16 * w + acc_row64(v)) * DP + 16 * b4 + col] -= acc[b4][v];
+    for (int v = 0; v < 4; ++v) S2[(16 * w + acc_row64(v)) * DP + 16 * b4 + col] -= acc[b4][v];
   __syncthreads();
   return true;
 }
@@ -369,9 +390,8 @@ __device__ __forceinline__ bool step_trailing(const InvJobDev& J, int k, int loc
 __device__ __forceinline__ void step_z(const InvJobDev& J, int k, int u, double* S0, double* S1,
                                        double* S2) {
   const int i = k + 1 + u / (k + 1), j = u % (k + 1);
-  load_tile(S0, tile_ptr(J.X, J.Np, k, k), J.Np);
-  load_tile(S1, tile_ptr(J.W, J.Np, i, k), J.Np);
-  if (j < k) load_tile(S2, tile_ptr(J.X, J.Np, k, j), J.Np);
+  load_tiles(S0, tile_ptr(J.X, J.Np, k, k), S1, tile_ptr(J.W, J.Np, i, k), j < k ? S2 : nullptr,
+             tile_ptr(J.X, J.Np, k, j), J.Np);
   __syncthreads();
   panel_tile_lds(S1, S0);  // C_i
   doublex4 acc[4];
@@ -391,8 +411,7 @@ __device__ __forceinline__ void step_z(const InvJobDev& J, int k, int u, double*
 // last row of X (k = T-1): X[k][j] = X[k][k] Z[k][j] -> W[k][j]
 __device__ __forceinline__ void step_last_row(const InvJobDev& J, int k, int j, double* S0,
                                               double* S1) {
-  load_tile(S0, tile_ptr(J.X, J.Np, k, k), J.Np);
-  load_tile(S1, tile_ptr(J.X, J.Np, k, j), J.Np);
+  load_tiles(S0, tile_ptr(J.X, J.Np, k, k), S1, tile_ptr(J.X, J.Np, k, j), nullptr, nullptr, J.Np);
   __syncthreads();
   doublex4 acc[4];
   gemm64<false>(S0, S1, acc);
@@ -410,7 +429,7 @@ __global__ __launch_bounds__(NTHREADS) void inv_step(InvArgs args) {
   const int local = blockIdx.x - args.begin[jb];
   const int nTrail = (T - k - 1) * (T - k) / 2;
   if (k < 0) {  // first diagonal tile
-    load_tile(S0, tile_ptr(J.W, J.Np, 0, 0), J.Np);
+    load_tile(S2, tile_ptr(J.W, J.Np, 0, 0), J.Np);
     __syncthreads();
   } else if (k == T - 1) {
     step_last_row(J, k, local, S0, S1);
@@ -423,7 +442,7 @@ __global__ __launch_bounds__(NTHREADS) void inv_step(InvArgs args) {
   }
   // the one diagonal factorisation of this step (single call site: stays inlined)
   const int d = k + 1;
-  diag_factor(S0, S1, dg);
+  diag_factor(S2, S1, dg);
   if (threadIdx.x == 0 && J.info) {
     for (int c = 0; c < NB; ++c) {
       const int g = d * NB + c;
@@ -463,8 +482,9 @@ __global__ __launch_bounds__(NTHREADS) void inv_update(InvArgs args) {
     const bool factor = (i == k + 1 && j == k + 1);
     doublex4 acc[4];
     if (k >= 0) {
-      load_tile(A, tile_ptr(J.W, J.Np, i, k), J.Np);
-      load_tile(B, tile_ptr(J.W, J.Np, j, k), J.Np);
+      // the factoring workgroup (i == j) prefetches its diagonal tile into Y
+      load_tiles(A, tile_ptr(J.W, J.Np, i, k), B, tile_ptr(J.W, J.Np, j, k), factor ? Y : nullptr,
+                 tile_ptr(J.W, J.Np, i, i), J.Np);
       __syncthreads();
       gemm64<true>(A, B, acc);
     }
@@ -474,17 +494,24 @@ __global__ __launch_bounds__(NTHREADS) void inv_update(InvArgs args) {
     }
     // the updated diagonal tile is consumed right here (never written back)
     __syncthreads();
-    load_tile(A, tile_ptr(J.W, J.Np, i, i), J.Np);
-    __syncthreads();
+    double* D = A;  // diagonal tile
+    double* Yo = Y;  // its factor's inverse
+    if (k >= 0) {
+      D = Y;
+      Yo = A;
+    } else {
+      load_tile(A, tile_ptr(J.W, J.Np, i, i), J.Np);
+      __syncthreads();
+    }
     if (k >= 0) {
       const int w = threadIdx.x >> 6, col = threadIdx.x & 15;
 #pragma unroll
       for (int b4 = 0; b4 < 4; ++b4)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) A[(16 * w + acc_row64(v)) * DP + 16 * b4 + col] -= acc[b4][v];
+        for (int v = 0; v < 4; ++v) D[(16 * w + acc_row64(v)) * DP + 16 * b4 + col] -= acc[b4][v];
       __syncthreads();
     }
-    diag_factor(A, Y, dg);
+    diag_factor(D, Yo, dg);
     if (threadIdx.x == 0 && J.info) {
       for (int c = 0; c < NB; ++c) {
         const int g = i * NB + c;
@@ -494,14 +521,13 @@ __global__ __launch_bounds__(NTHREADS) void inv_update(InvArgs args) {
         }
       }
     }
-    store_tile(tile_ptr(J.X, J.Np, i, i), Y, J.Np);
+    store_tile(tile_ptr(J.X, J.Np, i, i), Yo, J.Np);
     return;
   }
   // Z[i][j] -= C[i][k] X[k][j]   (i > k >= j)
   const int u = local - nTrail;
   const int i = k + 1 + u / (k + 1), j = u % (k + 1);
-  load_tile(A, tile_ptr(J.W, J.Np, i, k), J.Np);
-  load_tile(B, tile_ptr(J.X, J.Np, k, j), J.Np);
+  load_tiles(A, tile_ptr(J.W, J.Np, i, k), B, tile_ptr(J.X, J.Np, k, j), nullptr, nullptr, J.Np);
   __syncthreads();
   doublex4 acc[4];
   gemm64<false>(A, B, acc);
@@ -518,19 +544,18 @@ __global__ __launch_bounds__(NTHREADS) void inv_panel(InvArgs args) {
   const int k = args.step, T = J.T;
   const int local = blockIdx.x - args.begin[jb];
   const int nC = T - k - 1;
-  load_tile(Xk, tile_ptr(J.X, J.Np, k, k), J.Np);
   doublex4 acc[4];
   if (local < nC) {  // C[i][k] = R'[i][k] X[k][k]^T
     const int i = k + 1 + local;
     double* t = tile_ptr(J.W, J.Np, i, k);
-    load_tile(A, t, J.Np);
+    load_tiles(Xk, tile_ptr(J.X, J.Np, k, k), A, t, nullptr, nullptr, J.Np);
     __syncthreads();
     gemm64<true>(A, Xk, acc);
     store_acc_global(t, J.Np, acc, 1.0, false);
   } else {           // X[k][j] = X[k][k] Z[k][j]
     const int j = local - nC;
     double* t = tile_ptr(J.X, J.Np, k, j);
-    load_tile(A, t, J.Np);
+    load_tiles(Xk, tile_ptr(J.X, J.Np, k, k), A, t, nullptr, nullptr, J.Np);
     __syncthreads();
     gemm64<false>(Xk, A, acc);
     store_acc_global(t, J.Np, acc, 1.0, false);
@@ -557,8 +582,7 @@ __global__ __launch_bounds__(NTHREADS) void inv_xtx(InvArgs args) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = doublex4{0.0, 0.0, 0.0, 0.0};
   for (int m = a; m < J.T; ++m) {
-    load_tile(A, x_tile(J, m, a), J.Np);  // read transposed below
-    load_tile(B, x_tile(J, m, b), J.Np);
+    load_tiles(A, x_tile(J, m, a), B, x_tile(J, m, b), nullptr, nullptr, J.Np);  // A read transposed
     __syncthreads();
     const int i = lane & 15, kk = lane >> 4;
 #pragma unroll

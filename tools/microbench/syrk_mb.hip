@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+#include <algorithm>
 namespace kfac { void prof_begin(int, hipStream_t) {} void prof_end(int, hipStream_t) {} }
 using namespace kfac;
 
@@ -22,7 +23,48 @@ float time_tiles(TilesK k, FactorArgs la, int tasks, int reps) {
   return 1000.f * ms / reps;
 }
 
+// All-CU f32 MFMA burn (4 independent accumulators per wave, 4 waves per WG):
+// achievable rate and the core clock under this load (s_memtime vs the 100 MHz
+// s_memrealtime, sampled by wave 0 of block 0).
+template <int NA>
+__global__ __launch_bounds__(256) void mfma_burn(float* out, long long* clk, int iters) {
+  floatx16 acc[4];
+  for (int c = 0; c < 4; ++c)
+    for (int v = 0; v < 16; ++v) acc[c][v] = 0.f;
+  const float a = threadIdx.x * 1e-3f, b = blockIdx.x * 1e-3f;
+  long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < iters; ++i)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c % NA] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[c % NA], 0, 0, 0);
+  long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  float s = 0.f;
+  for (int c = 0; c < 4; ++c)
+    for (int v = 0; v < 16; ++v) s += acc[c][v];
+  if (s == 1234.5f) out[0] = s;
+  if (blockIdx.x == 0 && threadIdx.x == 0) { clk[0] = t1 - t0; clk[1] = r1 - r0; }
+}
+
 int main(int argc, char** argv) {
+  {
+    float* o; long long* ck;
+    (void)hipMalloc(&o, 4); (void)hipMalloc(&ck, 16);
+    for (int cfg = 0; cfg < 6; ++cfg) {
+      const int wgs = (cfg % 3 == 0) ? 256 : (cfg % 3 == 1) ? 512 : 1024, na = cfg < 3 ? 4 : 1;
+      const int iters = 800 * 256 / wgs;
+      auto k = na == 4 ? mfma_burn<4> : mfma_burn<1>;
+      hipLaunchKernelGGL(k, dim3(wgs), dim3(256), 0, 0, o, ck, iters);
+      hipEvent_t a, b; (void)hipEventCreate(&a); (void)hipEventCreate(&b);
+      (void)hipEventRecord(a, 0);
+      hipLaunchKernelGGL(k, dim3(wgs), dim3(256), 0, 0, o, ck, iters);
+      (void)hipEventRecord(b, 0); (void)hipEventSynchronize(b);
+      float ms; (void)hipEventElapsedTime(&ms, a, b);
+      long long h[2]; (void)hipMemcpy(h, ck, 16, hipMemcpyDeviceToHost);
+      const double fl = (double)wgs * 4 * iters * 4 * 32 * 32 * 2 * 2;
+      printf("acc/wave %d ", na);
+      printf("mfma burn %4d WGs: %7.2f us  %6.1f TF  clock %.2f GHz (wave0: %lld cyc / %lld ticks)\n", wgs,
+             ms * 1e3, fl / (ms * 1e-3) / 1e12, 0.1 * (double)h[0] / (double)h[1], h[0], h[1]);
+    }
+  }
   const int B = 4096;
   const int dims[4][2] = {{784, 1}, {128, 0}, {128, 1}, {10, 0}};  // cols, ones
   std::vector<float*> xs(4), Fs(4);
@@ -65,11 +107,9 @@ int main(int argc, char** argv) {
       la.job[i].glds = jobs[i].x.cols % 4 == 0;
     la.stagger = 5;
     struct V { const char* name; TilesK k; } vs[] = {
-        {"prod (BK32 x2 sched)", kfac_factor_tiles}, {"no sched", kfac_factor_tiles_t<32, 2, 0>},
-        {"setprio", kfac_factor_tiles_t<32, 2, 1>}, {"no stagger", kfac_factor_tiles_t<32, 2, 2 + 32>},
-        {"16x5 sub2", kfac_factor_tiles_t<16, 5, 2, 2>}, {"32x3", kfac_factor_tiles_t<32, 3, 2>},
-        {"no DMA", kfac_factor_tiles_t<32, 2, 2 + 4>}, {"no MFMA", kfac_factor_tiles_t<32, 2, 8>},
-        {"no DMA, no LDS reads", kfac_factor_tiles_t<32, 2, 4 + 16>}};
+        {"prod (BK32 x2 sched)", kfac_factor_tiles}, {"no stagger", kfac_factor_tiles_t<32, 2, 2 + 32>},
+        {"BK64 x2", kfac_factor_tiles_t<64, 2, 2>}, {"BK64 x2 nostag", kfac_factor_tiles_t<64, 2, 2 + 32>},
+        {"32x4 sub2", kfac_factor_tiles_t<32, 4, 2, 2>}};
     for (auto& v : vs) {
       float t0 = time_tiles(v.k, la, lt, 50);
       printf("target %5d tasks %5d | %-15s %6.2f us (%5.1f TF)\n", target, lt, v.name, t0, flops / t0 / 1e6);
