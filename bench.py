@@ -223,8 +223,11 @@ def main():
                 "frac": (achieved / MFMA_F32_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
                 "kernel": "kfac_factor_tiles", "launches": tiles_n,
                 "avg_launch_us": 1e3 * tiles_ms / max(tiles_n, 1),
-                "flops_per_launch": fpi * args.batch,
-                "algorithmic_bytes_per_launch": bytes_per_image(specs) * args.batch}
+                # a launch covers every queued update of the pass (multi-batch jobs):
+                # per-launch figures are the step's algorithmic totals / its launches
+                "flops_per_launch": fpi * args.images * args.steps / max(tiles_n, 1),
+                "algorithmic_bytes_per_launch": bytes_per_image(specs) * args.images * args.steps
+                                                / max(tiles_n, 1)}
     breakdown = {"factor_tiles_ms_per_step": tiles_ms / args.steps,
                  "factor_reduce_ms_per_step": red_ms / args.steps,
                  "invert_ms_per_step": inv_ms / args.steps,

@@ -35,7 +35,8 @@ class Operand(ctypes.Structure):
 
 class FactorJob(ctypes.Structure):
     _fields_ = [("x", Operand), ("alpha", c_f32), ("beta", c_f32), ("F", c_vp), ("ldF", c_i64),
-                ("acc", c_vp), ("acc_splits", c_i32), ("acc_beta", c_f32)]
+                ("acc", c_vp), ("acc_splits", c_i32), ("acc_beta", c_f32),
+                ("seg_ptrs", c_vp), ("nseg", c_i32), ("reserved2", c_i32)]
 
 
 class InvertJob(ctypes.Structure):
@@ -236,12 +237,11 @@ def kron_quadform(jobs, nb: int, abs_sum: bool, out: torch.Tensor):
 # ---------------------------------------------------------------- job builders
 def rowmajor_operand(x: torch.Tensor, has_ones: bool) -> Operand:
     """(rows, cols) row-major matrix, unit column stride (Linear a / g_rec)."""
-    assert x.dim() == 2 and x.stride(1) == 1
-    op = Operand()
-    op.ptr, op.layout, op.rows, op.cols = x.data_ptr(), ROWMAJOR, x.shape[0], x.shape[1]
-    op.ld = max(x.stride(0), x.shape[1])
-    op.has_ones = int(has_ones)
-    return op
+    rows, cols = x.shape
+    ld, unit = x.stride()
+    assert unit == 1
+    # positional constructor: one ctypes call instead of an attribute write per field
+    return Operand(x.data_ptr(), ROWMAJOR, cols, rows, int(has_ones), 0, max(ld, cols))
 
 
 def channel_operand(g: torch.Tensor) -> Operand:
@@ -280,12 +280,19 @@ def patch_operand(x: torch.Tensor, kernel, padding, stride, has_ones: bool) -> O
 
 
 def factor_job(op: Operand, F: torch.Tensor, alpha: float, beta: float) -> FactorJob:
-    j = FactorJob()
-    j.x = op
-    j.alpha, j.beta = alpha, beta
-    j.F = F.data_ptr()
-    j.ldF = F.stride(0)
-    return j
+    return FactorJob(op, alpha, beta, F.data_ptr(), F.stride(0))
+
+
+def segment_table(ptrs):
+    """HOST int64 array of batch base pointers for a multi-batch factor job
+    (kfac_factor_job.seg_ptrs).  kfac_factor_update reads it during the call and
+    passes the bases to the kernel as launch arguments: no device copy, no sync.
+    The caller keeps the returned array alive until the call returns."""
+    return (ctypes.c_int64 * len(ptrs))(*ptrs)
+
+
+def table_ptr(table) -> int:
+    return ctypes.addressof(table)
 
 
 def invert_job(F: torch.Tensor, out: torch.Tensor, scale: float, shift: float,

@@ -18,7 +18,8 @@
 
 namespace kfac {
 
-constexpr int MAXJ = 16;  // factor jobs per launch (kernarg budget: ~3 KB of 4 KB)
+constexpr int MAXJ = 16;  // factor jobs per launch (kernarg budget: ~3.2 KB of 4 KB)
+constexpr int KSEG = 64;  // batch base pointers per launch (multi-batch jobs; +512 B)
 
 struct FactorJobDev {
   OpDev x;
@@ -26,7 +27,10 @@ struct FactorJobDev {
   float* F;
   int64_t ldF;
   float* slab;       // this job's slabs: tiles*splits x 64 x 64
-  int64_t chunk;     // rows per split (multiple of BK)
+  int seg_off;       // multi-batch job: its batch bases are FactorArgs::segs[seg_off..] (else -1)
+  int64_t chunk;     // BK-row stages per split
+  int64_t nst;       // stages of the job: nseg * sps
+  int sps, nseg;     // stages per batch (a stage never straddles two batches), batches
   int n, t, splits;  // factor edge, tiles per edge, K-splits
   int task_begin;    // first global task of this job
   int glds;          // row-major, 16-byte-aligned rows: LDS-DMA kernel
@@ -36,6 +40,7 @@ struct FactorJobDev {
 };
 
 struct FactorArgs {
+  const float* segs[KSEG];  // batch bases of the multi-batch jobs (kernel arguments: no copy)
   int njobs;
   int stagger;  // start delay per dispatch round, in 512-cycle s_sleep(8) units
   int task_end[MAXJ];
@@ -65,6 +70,28 @@ __device__ __forceinline__ void put_partial(const FactorJobDev& J, const floatx1
   for (int v = 0; v < 16; ++v) *at(v) = fmaf(J.sbeta, old[v], J.alpha * acc[v]);
 }
 
+// K is walked in BK-row stages; stage s of a job is rows [k, k + BK) of batch
+// `seg` (s = seg * sps + k / BK), so a multi-batch job reads each batch in place.
+// `segs` = FactorArgs::segs (kernel-argument memory; never null: a conditional
+// null pointer here makes the compiler copy the whole argument block to scratch).
+__device__ __forceinline__ const float* seg_base(const FactorJobDev& J, const float* const* segs,
+                                                 int seg) {
+  return J.seg_off >= 0 ? segs[J.seg_off + seg] : J.x.ptr;
+}
+
+struct StageCursor {
+  int seg;
+  int64_t k;  // first row of the stage within batch `seg`
+  __device__ __forceinline__ void init(const FactorJobDev& J, int64_t s) {
+    seg = (int)(s / J.sps);
+    k = (s - (int64_t)seg * J.sps) * BK;
+  }
+  __device__ __forceinline__ void next(int64_t rows) {
+    k += BK;
+    if (k >= rows) { k = 0; ++seg; }
+  }
+};
+
 // Narrow factors (n <= 32): the 4 waves hold partial sums of quadrant (0,0) over
 // disjoint K subsets; sum them through LDS in wave order (deterministic) and store
 // the quadrant.  `lds` is free (the caller's stage loop has ended with a barrier).
@@ -86,13 +113,14 @@ __device__ __forceinline__ void store_narrow(const FactorJobDev& J, float* out, 
 }
 
 template <int LAYOUT>
-__device__ __forceinline__ void factor_task(const FactorJobDev& J, int local, float* lds) {
+__device__ __forceinline__ void factor_task(const FactorJobDev& J, const float* const* segs, int local,
+                                            float* lds) {
   // tile-major order: a tile's splits are consecutive tasks (one XCD; see the reduce)
   const int tile = local / J.splits, split = local - tile * J.splits;
   int ti, tj;
   tri_decode(tile, ti, tj);
-  const int64_t k0 = (int64_t)split * J.chunk;
-  const int64_t k1 = min(J.x.rows, k0 + J.chunk);
+  const int64_t s0 = (int64_t)split * J.chunk;
+  const int64_t s1 = min(J.nst, s0 + J.chunk);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int qi = wave >> 1, qj = wave & 1;
   const bool diag = ti == tj;
@@ -103,8 +131,24 @@ __device__ __forceinline__ void factor_task(const FactorJobDev& J, int local, fl
 #pragma unroll
   for (int v = 0; v < 16; ++v) acc[v] = 0.f;
   const bool narrow = J.n <= 32;  // one 32x32 quadrant: the 4 waves split K instead
-  contract_tile<LAYOUT, LAYOUT>(J.x, ti * TILE, J.x, tj * TILE, k0, k1, diag, active, lds, acc,
-                                narrow);
+  if constexpr (LAYOUT == KFAC_ROWMAJOR) {
+    // one pipelined contraction per batch piece of this split's stage range
+    StageCursor c;
+    c.init(J, s0);
+    for (int64_t s = s0; s < s1;) {
+      const int64_t here = min(s1 - s, (int64_t)J.sps - c.k / BK);
+      contract_tile<LAYOUT, LAYOUT>(J.x, ti * TILE, J.x, tj * TILE, c.k,
+                                    min(J.x.rows, c.k + here * BK), diag, active, lds, acc, narrow,
+                                    seg_base(J, segs, c.seg));
+      s += here;
+      c.seg += 1;
+      c.k = 0;
+    }
+  } else {
+    // channel-major / im2col jobs are single-batch (validate()): stage s = rows [s*BK, ..)
+    contract_tile<LAYOUT, LAYOUT>(J.x, ti * TILE, J.x, tj * TILE, s0 * BK, min(J.x.rows, s1 * BK),
+                                  diag, active, lds, acc, narrow);
+  }
   if (narrow) {
     store_narrow(J, J.slab + ((size_t)tile * J.splits + split) * TILE * TILE, acc, lds);
     return;
@@ -129,14 +173,13 @@ __device__ __forceinline__ void factor_task(const FactorJobDev& J, int local, fl
 template <int GBK>
 struct GldsPanel {
   static constexpr int NCH = GBK / 16;
-  const float* base;
   int64_t ld, kend;
   int ch[NCH];       // this thread's 16-byte chunks of a panel (GBK x 16 chunks)
   int col[NCH];      // first column of each chunk
   bool real[NCH];    // chunk holds matrix data (else fill)
   float4 fill[NCH];  // fill value of a non-real chunk (ones column -> 1)
   __device__ __forceinline__ void init(const OpDev& op, int col0, int w, int lane, int64_t k_end) {
-    base = op.ptr; ld = op.ld; kend = k_end;
+    ld = op.ld; kend = k_end;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       ch[i] = (w * NCH + i) * 64 + lane;
@@ -148,8 +191,8 @@ struct GldsPanel {
       fill[i] = make_float4(f[0], f[1], f[2], f[3]);
     }
   }
-  // issue the LDS-DMA loads of stage rows [k, k+GBK) into `slot` (panel base)
-  __device__ __forceinline__ void issue(int64_t k, float* slot, int w) const {
+  // issue the LDS-DMA loads of rows [k, k+GBK) of the batch at `base` into `slot`
+  __device__ __forceinline__ void issue(const float* base, int64_t k, float* slot, int w) const {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int64_t row = k + (ch[i] >> 4);
@@ -197,13 +240,14 @@ __device__ __forceinline__ void stage_barrier() {
 // NACC independent accumulators per wave (k-steps interleaved) to keep back-to-back
 // MFMAs off the 64-cycle dependent-accumulator latency.
 template <int GBK, int NSLOT, int NACC, int MODE = 0, int SUB = 1>
-__device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, int local, float* lds) {
+__device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, const float* const* segs,
+                                                 int local, float* lds) {
   static_assert(NSLOT >= 2 * SUB, "ring must hold the computed step and the next one");
   const int tile = local / J.splits, split = local - tile * J.splits;
   int ti, tj;
   tri_decode(tile, ti, tj);
-  const int64_t k0 = (int64_t)split * J.chunk;
-  const int64_t k1 = min(J.x.rows, k0 + J.chunk);
+  const int64_t s0 = (int64_t)split * J.chunk;
+  const int64_t s1 = min(J.nst, s0 + J.chunk);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int qi = wave >> 1, qj = wave & 1;
   const bool same = ti == tj;
@@ -215,21 +259,31 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, int loca
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[c][v] = 0.f;
 
-  if (k1 > k0 && !(MODE & 64)) {
+  static_assert(GBK == BK, "a ring slot is one planner stage");
+  if (s1 > s0 && !(MODE & 64)) {
     // ring of NSLOT slots of GBK rows; one barrier per step of SUB slots, so
-    // NSLOT - SUB slots are in flight while a step computes
+    // NSLOT - SUB slots are in flight while a step computes.  Slots are issued and
+    // landed in stage order, each walked by its own cursor across batch boundaries.
     constexpr int GSLOT = 2 * GBK * TILE;  // floats per ring slot (A and B panels)
+    const int64_t rows = J.x.rows;
     GldsPanel<GBK> pa, pb;
-    pa.init(J.x, ti * TILE, wave, lane, k1);
-    pb.init(J.x, tj * TILE, wave, lane, k1);
-    const int ns = (int)((k1 - k0 + GBK - 1) / GBK);  // slots of this task
+    pa.init(J.x, ti * TILE, wave, lane, rows);
+    pb.init(J.x, tj * TILE, wave, lane, rows);
+    const int ns = (int)(s1 - s0);  // slots of this task
     const int nstep = (ns + SUB - 1) / SUB;
     const int per = (same ? 1 : 2) * GldsPanel<GBK>::NCH;  // LDS-DMA instructions per slot per thread
+    StageCursor ic, fc;  // next slot to issue / to land
+    ic.init(J, s0);
+    fc = ic;
+    const float* ibase = seg_base(J, segs, ic.seg);
     auto issue = [&](int sl) {
       if (MODE & 4) return;
       float* slot = lds + (sl % NSLOT) * GSLOT;
-      pa.issue(k0 + (int64_t)sl * GBK, slot, wave);
-      if (!same) pb.issue(k0 + (int64_t)sl * GBK, slot + GBK * TILE, wave);
+      pa.issue(ibase, ic.k, slot, wave);
+      if (!same) pb.issue(ibase, ic.k, slot + GBK * TILE, wave);
+      const int seg = ic.seg;
+      ic.next(rows);
+      if (ic.seg != seg && sl + 1 < ns) ibase = seg_base(J, segs, ic.seg);
     };
 #pragma unroll
     for (int p0 = 0; p0 < NSLOT - SUB; ++p0)
@@ -245,9 +299,9 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, int loca
         const int sl = SUB * st + u;
         if (sl < ns) {
           float* slot = lds + (sl % NSLOT) * GSLOT;
-          const int64_t kst = k0 + (int64_t)sl * GBK;
-          pa.fixup(kst, slot);
-          if (!same) pb.fixup(kst, slot + GBK * TILE);
+          pa.fixup(fc.k, slot);
+          if (!same) pb.fixup(fc.k, slot + GBK * TILE);
+          fc.next(rows);
         }
       }
       stage_barrier();  // step st visible to all waves; everyone is done with step st-1's slots
@@ -317,11 +371,13 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, int loca
   put_partial(J, acc[0], [&](int v) { return &out[acc_row(v, lane) * TILE + (lane & 31)]; });
 }
 
-// One launch per grouped update: each task takes the LDS-DMA path when its job's
-// operand allows it, else the register-staged path for its layout.
-template <int GBK, int NSLOT, int MODE = 0, int SUB = 1>
+// One launch per grouped update.  The row-major family (FAMILY = KFAC_ROWMAJOR)
+// takes the LDS-DMA path when a job's operand allows it, else the register-staged
+// row-major path; channel-major and im2col jobs get launches (and register budgets)
+// of their own, instantiated per layout.
+template <int GBK, int NSLOT, int MODE = 0, int SUB = 1, int FAMILY = KFAC_ROWMAJOR>
 __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs args) {
-  constexpr int RING = NSLOT * 2 * GBK * TILE;
+  constexpr int RING = FAMILY == KFAC_ROWMAJOR ? NSLOT * 2 * GBK * TILE : 0;
   __shared__ __attribute__((aligned(16))) float lds[(4 * PANEL > RING) ? 4 * PANEL : RING];
   // Workgroups of later dispatch rounds (blockIdx / 256: the ~4 sharing a CU) start a
   // fraction of a stage later, so their DMA waits and barriers interleave instead of
@@ -333,20 +389,22 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
   while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
   const FactorJobDev& J = args.job[j];
   const int local = task - J.task_begin;
-  if (J.glds) {
-    factor_task_glds<GBK, NSLOT, 1, MODE, SUB>(J, local, lds);
-    return;
-  }
-  switch (J.x.layout) {
-    case KFAC_ROWMAJOR: factor_task<KFAC_ROWMAJOR>(J, local, lds); break;
-    case KFAC_CHANNEL: factor_task<KFAC_CHANNEL>(J, local, lds); break;
-    default: factor_task<KFAC_PATCH>(J, local, lds); break;
+  if constexpr (FAMILY == KFAC_ROWMAJOR) {
+    const float* const* segs = args.segs;
+    if (J.glds)
+      factor_task_glds<GBK, NSLOT, 1, MODE, SUB>(J, segs, local, lds);
+    else
+      factor_task<KFAC_ROWMAJOR>(J, segs, local, lds);
+  } else {
+    factor_task<FAMILY>(J, nullptr, local, lds);
   }
 }
 
 // production configuration: 32-row stages, 2-slot ring (one stage in flight),
 // DS reads interleaved with the MFMAs (MODE 2: -1.2 us of 42 on the MLP update)
 #define kfac_factor_tiles kfac_factor_tiles_t<32, 2, 2>
+#define kfac_factor_tiles_channel kfac_factor_tiles_t<32, 2, 2, 1, KFAC_CHANNEL>
+#define kfac_factor_tiles_patch kfac_factor_tiles_t<32, 2, 2, 1, KFAC_PATCH>
 
 // One block = one 4-row strip of one 64x64 tile.  Each float4 of the strip is
 // summed by 4 threads over interleaved splits (part p: splits p, p+4, ...); the
@@ -432,33 +490,57 @@ struct Plan {
 
 static int factor_n(const kfac_factor_job& j) { return j.x.cols + (j.x.has_ones ? 1 : 0); }
 
-// Split K so that the whole grouped launch has ~4 tasks per CU (256 CUs) but
-// every task still runs >= 256 rows of MFMA work.  A job with a deferred-reduction
-// accumulator keeps the accumulator's split count (its layout): its K range is cut
-// into that many equal chunks (trailing splits of a smaller batch may be empty and
-// then contribute zero).
+// K stages (BK rows each, never straddling two batches) of a job.
+static int64_t job_sps(const kfac_factor_job& j) { return std::max<int64_t>(1, cdiv(j.x.rows, BK)); }
+static int job_nseg(const kfac_factor_job& j) { return j.nseg > 1 ? j.nseg : 1; }
+static int64_t job_stages(const kfac_factor_job& j) { return job_sps(j) * job_nseg(j); }
+
+// Split K so that the grouped launch fills the chip's workgroup slots (256 CUs x 4
+// resident workgroups) in as few dispatch rounds as possible with every task still
+// running >= 8 stages (256 rows) of MFMA work.  One chunk length c (stages) is used
+// for every job; tasks(c) = sum_j tiles_j * ceil(stages_j / c) falls with c, and the
+// modelled time is (c + prologue/epilogue) * rounds: the smallest c that fits r
+// rounds is found by bisection for r = 1..4 and the cheapest r wins.
+// A job with a deferred-reduction accumulator keeps the accumulator's split count
+// (its layout): its stage range is cut into that many equal chunks (trailing splits
+// of a smaller batch may be empty and then contribute zero).
 static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
-                      int64_t target_tasks = 1024) {
-  int64_t work = 0;
-  for (int i = 0; i < njobs; ++i) {
-    const int t = (int)cdiv(factor_n(jobs[i]), TILE);
-    work += (int64_t)t * (t + 1) / 2 * cdiv(jobs[i].x.rows, BK);
+                      int64_t slots = 1024) {
+  constexpr int64_t MIN_CHUNK = 8, OVERHEAD = 4;  // stages; ~per-task fixed cost in stages
+  int64_t max_steps = 1;
+  for (int i = 0; i < njobs; ++i) max_steps = std::max(max_steps, job_stages(jobs[i]));
+  auto tasks_at = [&](int64_t c) {
+    int64_t n = 0;
+    for (int i = 0; i < njobs; ++i) {
+      const int64_t t = cdiv(factor_n(jobs[i]), TILE);
+      n += t * (t + 1) / 2 * cdiv(job_stages(jobs[i]), c);
+    }
+    return n;
+  };
+  int64_t best_c = std::max(MIN_CHUNK, max_steps), best_cost = -1;
+  for (int64_t r = 1; r <= 4; ++r) {
+    int64_t lo = MIN_CHUNK, hi = std::max(MIN_CHUNK, max_steps);
+    if (tasks_at(hi) > r * slots) continue;  // even one split per tile needs more rounds
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) / 2;
+      if (tasks_at(mid) <= r * slots) hi = mid; else lo = mid + 1;
+    }
+    const int64_t cost = (lo + OVERHEAD) * r;
+    if (best_cost < 0 || cost < best_cost) { best_cost = cost; best_c = lo; }
   }
-  int64_t chunk_steps = std::max<int64_t>(8, cdiv(work, target_tasks));  // in BK units
   for (int i = 0; i < njobs; ++i) {
     const int t = (int)cdiv(factor_n(jobs[i]), TILE);
     Plan& p = plans[i];
     p.tiles = t * (t + 1) / 2;
-    const int64_t steps = std::max<int64_t>(1, cdiv(jobs[i].x.rows, BK));
+    const int64_t steps = job_stages(jobs[i]);
     if (jobs[i].acc) {
       p.splits = jobs[i].acc_splits;
-      p.chunk = cdiv(steps, (int64_t)p.splits) * BK;
+      p.chunk = cdiv(steps, (int64_t)p.splits);
       p.slab_bytes = 0;  // partials go to the caller's accumulator
       continue;
     }
-    const int64_t cs = std::min(chunk_steps, steps);
-    p.chunk = cs * BK;
-    p.splits = (int)cdiv(steps, cs);
+    p.splits = (int)cdiv(steps, best_c);
+    p.chunk = cdiv(steps, (int64_t)p.splits);
     p.slab_bytes = align_up((size_t)p.tiles * p.splits * TILE * TILE * sizeof(float), 256);
   }
 }
@@ -492,6 +574,10 @@ static void fill_dev(FactorJobDev& d, const kfac_factor_job& jb) {
   d.t = (int)cdiv(d.n, TILE);
   d.accum = jb.acc != nullptr;
   d.sbeta = jb.acc_beta;
+  d.seg_off = -1;  // factor_group() places multi-batch bases
+  d.nseg = job_nseg(jb);
+  d.sps = (int)job_sps(jb);
+  d.nst = job_stages(jb);
 }
 
 // One reduce launch over `njobs` jobs whose slabs are described by d.slab/d.splits.
@@ -510,7 +596,7 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
   FactorArgs red{};  // the reduce launch: jobs reduced now (no accumulator)
   args.njobs = njobs;
   args.stagger = 5;
-  int tasks = 0, rtiles = 0;
+  int tasks = 0, rtiles = 0, nsegs = 0;
   size_t off = 0;
   for (int i = 0; i < njobs; ++i) {
     const kfac_factor_job& jb = jobs[i];
@@ -521,6 +607,11 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
              (reinterpret_cast<uintptr_t>(jb.x.ptr) % 16) == 0;
     d.splits = plans[i].splits;
     d.chunk = plans[i].chunk;
+    if (d.nseg > 1) {  // kfac_factor_update keeps a launch within KSEG batch bases
+      const float* const* bases = reinterpret_cast<const float* const*>(jb.seg_ptrs);
+      d.seg_off = nsegs;
+      for (int s = 0; s < d.nseg; ++s) args.segs[nsegs++] = bases[s];
+    }
     if (jb.acc) {
       d.slab = jb.acc;
     } else {
@@ -540,7 +631,17 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
   if (tasks == 0) return KFAC_OK;
   {
     ProfScope ps(KFAC_PROF_FACTOR_TILES, stream);
-    hipLaunchKernelGGL(kfac_factor_tiles, dim3(tasks), dim3(NTHREADS), 0, stream, args);
+    // launch_groups() gives every channel-major / im2col job a group of its own
+    switch (jobs[0].x.layout) {
+      case KFAC_CHANNEL:
+        hipLaunchKernelGGL(kfac_factor_tiles_channel, dim3(tasks), dim3(NTHREADS), 0, stream, args);
+        break;
+      case KFAC_PATCH:
+        hipLaunchKernelGGL(kfac_factor_tiles_patch, dim3(tasks), dim3(NTHREADS), 0, stream, args);
+        break;
+      default:
+        hipLaunchKernelGGL(kfac_factor_tiles, dim3(tasks), dim3(NTHREADS), 0, stream, args);
+    }
     KFAC_CHECK_LAUNCH();
   }
   launch_reduce(red, rtiles, stream);
@@ -604,6 +705,9 @@ static int validate(const kfac_factor_job* jobs, int njobs) {
     if (!valid_operand(j.x) || !j.F || j.ldF < factor_n(j)) return KFAC_EINVAL;
     if ((int64_t)factor_n(j) > (int64_t)1 << 20) return KFAC_EINVAL;
     if (j.acc && (j.acc_splits <= 0 || j.acc_splits > (1 << 20))) return KFAC_EINVAL;
+    if (j.nseg < 0 || (j.nseg > 1 && (!j.seg_ptrs || j.x.layout != KFAC_ROWMAJOR)) ||
+        job_sps(j) > (1 << 30))
+      return KFAC_EINVAL;
   }
   return KFAC_OK;
 }
@@ -638,9 +742,46 @@ extern "C" int kfac_factor_update(const kfac_factor_job* jobs, int njobs, void* 
   std::vector<std::pair<int, int>> groups;
   launch_groups(jobs, njobs, sorted, order, groups);
   for (const auto& g : groups) {
-    const int rc = factor_group(sorted.data() + g.first, g.second, (char*)workspace,
-                                workspace_bytes, (hipStream_t)stream);
-    if (rc != KFAC_OK) return rc;
+    const kfac_factor_job* gj = sorted.data() + g.first;
+    int multi = 0, maxseg = 1, total = 0;
+    for (int k = 0; k < g.second; ++k)
+      if (job_nseg(gj[k]) > 1) {
+        ++multi;
+        maxseg = std::max(maxseg, gj[k].nseg);
+        total += gj[k].nseg;
+      }
+    if (total <= KSEG) {
+      const int rc = factor_group(gj, g.second, (char*)workspace, workspace_bytes, (hipStream_t)stream);
+      if (rc != KFAC_OK) return rc;
+      continue;
+    }
+    // more batch bases than one launch's kernel arguments hold: rounds of S batches
+    // per multi-batch job, each round adding to what the previous ones wrote
+    const int S = KSEG / multi;  // >= KSEG / MAXJ = 4
+    for (int r = 0; r * S < maxseg; ++r) {
+      std::vector<kfac_factor_job> sub;
+      for (int k = 0; k < g.second; ++k) {
+        kfac_factor_job j = gj[k];
+        if (job_nseg(j) > 1) {
+          const int b0 = r * S;
+          if (b0 >= j.nseg) continue;
+          const float* const* bases = reinterpret_cast<const float* const*>(j.seg_ptrs) + b0;
+          j.seg_ptrs = bases;
+          j.nseg = std::min(S, j.nseg - b0);
+          j.x.ptr = bases[0];
+        } else if (r > 0) {
+          continue;
+        }
+        if (r > 0) {
+          if (j.acc) j.acc_beta = 1.f;
+          else j.beta = 1.f;
+        }
+        sub.push_back(j);
+      }
+      const int rc = factor_group(sub.data(), (int)sub.size(), (char*)workspace, workspace_bytes,
+                                  (hipStream_t)stream);
+      if (rc != KFAC_OK) return rc;
+    }
   }
   return KFAC_OK;
 }

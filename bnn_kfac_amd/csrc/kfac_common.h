@@ -80,8 +80,9 @@ struct Panel<KFAC_ROWMAJOR> {
   int64_t ld, kend;
   int col, c4, r0, cols, ones;
   bool vec;
-  __device__ __forceinline__ void init(const OpDev& op, int col0, int tid, int64_t k_end, int64_t) {
-    base = op.ptr; ld = op.ld; kend = k_end; cols = op.cols; ones = op.ones;
+  __device__ __forceinline__ void init(const OpDev& op, const float* base_, int col0, int tid,
+                                       int64_t k_end, int64_t) {
+    base = base_; ld = op.ld; kend = k_end; cols = op.cols; ones = op.ones;
     c4 = (tid & 15) * 4; r0 = tid >> 4; col = col0 + c4;
     vec = (col + 3 < cols) && ((ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(base) & 15) == 0);
   }
@@ -124,9 +125,9 @@ struct Panel<KFAC_CHANNEL> {
   const float* base;
   int64_t L, sB, kend, b, l;  // (b, l) of row k + r for the next load
   int r, c0, col0, cols, ones;
-  __device__ __forceinline__ void init(const OpDev& op, int col0_, int tid, int64_t k_end,
-                                       int64_t k_first) {
-    base = op.ptr; L = op.L; sB = op.sB; kend = k_end; cols = op.cols; ones = op.ones;
+  __device__ __forceinline__ void init(const OpDev& op, const float* base_, int col0_, int tid,
+                                       int64_t k_end, int64_t k_first) {
+    base = base_; L = op.L; sB = op.sB; kend = k_end; cols = op.cols; ones = op.ones;
     r = tid & 31; c0 = tid >> 5; col0 = col0_;
     const int64_t row = k_first + r;
     b = row / L;
@@ -160,9 +161,9 @@ struct Panel<KFAC_PATCH> {
   int r, c0, H, W, Ho, Wo, sh, sw, ph, pw, oh, ow;
   int coff[8];
   int kij[8];  // (ki << 16) | kj, or KZERO / KONES
-  __device__ __forceinline__ void init(const OpDev& op, int col0, int tid, int64_t k_end,
-                                       int64_t k_first) {
-    base = op.ptr; sB = op.sB; kend = k_end;
+  __device__ __forceinline__ void init(const OpDev& op, const float* base_, int col0, int tid,
+                                       int64_t k_end, int64_t k_first) {
+    base = base_; sB = op.sB; kend = k_end;
     H = op.H; W = op.W; Ho = op.Ho; Wo = op.Wo; sh = op.sh; sw = op.sw; ph = op.ph; pw = op.pw;
     r = tid & 31; c0 = tid >> 5;
     const int64_t row = k_first + r;
@@ -221,10 +222,13 @@ struct Panel<KFAC_PATCH> {
 // `active` = this wave's quadrant is needed (waves always join staging/barriers).
 // `narrow`: only quadrant (0,0) is needed (factor edge <= 32): every wave computes
 // it over its own quarter of each stage's K rows (the caller sums the 4 partials).
+// `base` (null: opA.ptr / opB.ptr) replaces both operands' base pointer (one batch of
+// a multi-batch job; then opA and opB are the same operand).
 template <int LA, int LB>
 __device__ __forceinline__ void contract_tile(const OpDev& opA, int i0, const OpDev& opB, int j0,
                                               int64_t k0, int64_t k1, bool same, bool active,
-                                              float* lds, floatx16& acc, bool narrow = false) {
+                                              float* lds, floatx16& acc, bool narrow = false,
+                                              const float* base = nullptr) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int qi = narrow ? 0 : wave >> 1, qj = narrow ? 0 : wave & 1;
@@ -232,8 +236,8 @@ __device__ __forceinline__ void contract_tile(const OpDev& opA, int i0, const Op
 
   Panel<LA> pa;
   Panel<LB> pb;
-  pa.init(opA, i0, tid, k1, k0);
-  pb.init(opB, j0, tid, k1, k0);
+  pa.init(opA, base ? base : opA.ptr, i0, tid, k1, k0);
+  pb.init(opB, base ? base : opB.ptr, j0, tid, k1, k0);
   float va[8], vb[8];
 
   // buffer c: A panel at lds + 2*c*PANEL, B panel right after it

@@ -151,25 +151,44 @@ class KFAC(Curvature):
         self._packed = None      # flat fp32 device buffer holding every factor
         self._packed_views = {}  # layer -> (A view, G view)
         self._layer_list = list(self.record)
-        # Deferred reduction (kfac_factor_flush): updates keep each factor's split-K
-        # partial tiles in device accumulators; the reduce into `state` runs once,
-        # when the state is next read (invert / save / `state` / all-reduce).
+        # Deferred execution (flush() completes it; every `state` read flushes):
+        # * queued updates: update() resolves each batch's factor jobs and keeps the
+        #   records alive (no copy); up to `defer_batches` updates are then launched
+        #   together, row-major factors as ONE multi-batch MFMA job each (K walks all
+        #   queued batches in place), so a pass costs ~one launch instead of one per batch;
+        # * deferred reduction (kfac_factor_flush): the launches keep each factor's
+        #   split-K partial tiles in device accumulators; the reduce into `state` runs
+        #   once, when the state is next read (invert / save / `state` / all-reduce).
         self.defer_reduce = True
-        self._acc_buf = None     # grow-only device buffer of the accumulators
+        self.defer_batches = 64
+        self._queue = []         # per queued update: (jobs, operand pointers, kept records,
+                                 # their _version, device, merge key)
+        self._launch_at = 1      # queue length that triggers the next launch
+        self._fast = None        # job templates of the last slow-path update (see _remember)
+        self._acc_buf = None     # device buffer of the accumulators
+        self._acc_map = None     # F pointer -> (acc pointer, splits) of the pending cycle
+        self._acc_live = set()   # F pointers already written in the pending cycle
         self._acc_flush = None   # flush jobs of the pending cycle (None: nothing pending)
         self._acc_device = None
 
     def reset(self):
         """Forget the accumulated factors (start a new data pass); device buffers are kept."""
-        self._acc_flush = None
+        self._queue = []
+        self._launch_at = 1
+        self._fast = None
+        self._acc_flush = self._acc_map = None
         self._state = dict()
         self.inv_state = dict()
 
     def flush(self):
-        """Reduce the pending accumulators into the factors (one launch; async)."""
+        """Launch queued updates, then reduce the pending accumulators into the
+        factors (async; one reduce launch)."""
+        if getattr(self, "_queue", None):
+            self._launch_queue()
+        self._launch_at = 1
         jobs = getattr(self, "_acc_flush", None)
         if jobs:
-            self._acc_flush = None
+            self._acc_flush = self._acc_map = None
             N.factor_flush(jobs, self._acc_device)
 
     # curvatures.py:319-323
@@ -203,16 +222,18 @@ class KFAC(Curvature):
             opG = N.channel_operand(g)
             keep = (x, g)
         else:
-            a = forward.detach()
-            g = backward.detach()
-            if a.dim() > 2 or g.dim() > 2:
-                raise RuntimeError("t() expects a tensor with <= 2 dimensions, but self is "
-                                   f"{max(a.dim(), g.dim())}D")
-            a = a.reshape(1, -1) if a.dim() == 1 else a
-            g = g.reshape(1, -1) if g.dim() == 1 else g
-            if a.stride(-1) != 1:
+            # only data pointers are read: no detach() needed
+            a, g = forward, backward
+            da, dg = a.dim(), g.dim()
+            if da != 2 or dg != 2:
+                if da > 2 or dg > 2:
+                    raise RuntimeError("t() expects a tensor with <= 2 dimensions, but self is "
+                                       f"{max(da, dg)}D")
+                a = a.reshape(1, -1) if da == 1 else a
+                g = g.reshape(1, -1) if dg == 1 else g
+            if a.stride(1) != 1:
                 a = a.contiguous()
-            if g.stride(-1) != 1:
+            if g.stride(1) != 1:
                 g = g.contiguous()
             opA = N.rowmajor_operand(a, has_bias)
             opG = N.rowmajor_operand(g, False)
@@ -262,6 +283,11 @@ class KFAC(Curvature):
     def update(self, batch_size: int):
         """Accumulate this batch's factors for every selected layer
         (curvatures.py:325-365; `batch_size` is unused there too)."""
+        if self.defer_reduce and self._fast is not None:
+            entry = self._fast_entry()
+            if entry is not None:
+                self._enqueue(entry)
+                return
         prepared = []
         for layer in self._layers():
             forward, backward = self.record[layer]
@@ -274,44 +300,157 @@ class KFAC(Curvature):
         device = prepared[0][5][0].device
         if any(layer not in self._state for layer, *_ in prepared):
             self._ensure_packed([(p[0], p[3], p[4]) for p in prepared], device)
-        jobs = []
-        for layer, opA, opG, nA, nG, _keep in prepared:
+        jobs, keep = [], []
+        for layer, opA, opG, nA, nG, kept in prepared:
             A, G, beta = self._target(layer, nA, nG, device)
             jobs.append(N.factor_job(opA, A, self._alpha(opA), beta))
             jobs.append(N.factor_job(opG, G, self._alpha(opG), beta))
-        if self.defer_reduce:
+            keep.extend(kept)
+        if not self.defer_reduce:
+            N.factor_update(jobs, device)
+            return
+        self._remember(prepared, jobs, device)
+        # merge key: the fast path's job templates when later updates can reuse them
+        # (they differ from `jobs` only in beta and pointers), else this update alone
+        key = self._fast[2] if self._fast is not None else tuple(jobs)
+        self._enqueue((tuple(jobs), tuple(j.x.ptr for j in jobs), keep,
+                       [t._version for t in keep], device, key))
+
+    # Fast path: a later update whose records have the same shapes, strides, dtype and
+    # device as the last slow-path one, and whose targets are still the same `state`
+    # entries, reuses that update's job templates (beta 1: the factors now exist) and
+    # only reads the records' data pointers.
+    @staticmethod
+    def _signature(t):
+        return t.shape, t.stride(), t.dtype, t.device
+
+    def _remember(self, prepared, jobs, device):
+        self._fast = None
+        spec = []
+        for layer, _opA, _opG, _nA, _nG, kept in prepared:
+            forward, backward = self.record[layer]
+            if kept[0] is not forward or kept[1] is not backward:
+                return  # a reshaped / made-contiguous record: stay on the slow path
+            lst = self._state[layer]
+            spec.append((layer, self._signature(forward), self._signature(backward), lst, lst[0], lst[1]))
+        tmpl = []
+        for j in jobs:
+            t = N.FactorJob.from_buffer_copy(j)
+            t.beta = 1.0
+            tmpl.append(t)
+        self._fast = (getattr(self, "_scale", 1.0), spec, tuple(tmpl), device)
+
+    def _fast_entry(self):
+        scale, spec, tmpl, device = self._fast
+        if getattr(self, "_scale", 1.0) != scale:
+            return None
+        record, state, sig = self.record, self._state, self._signature
+        ptrs, keep = [], []
+        for layer, sig_f, sig_b, lst, A, G in spec:
+            forward, backward = record[layer]
+            if forward is None or backward is None or sig(forward) != sig_f or sig(backward) != sig_b:
+                return None
+            if state.get(layer) is not lst or lst[0] is not A or lst[1] is not G:
+                return None
+            ptrs.append(forward.data_ptr())
+            ptrs.append(backward.data_ptr())
+            keep.append(forward)
+            keep.append(backward)
+        return tmpl, tuple(ptrs), keep, [t._version for t in keep], device, tmpl
+
+    def _enqueue(self, entry):
+        """Queue one update: (jobs, operand pointers, records kept alive, their
+        _version, device, merge key)."""
+        if self._queue and self._queue[0][4] != entry[4]:
+            self._launch_queue()
+        self._queue.append(entry)
+        # launch sizes double from 1 up to defer_batches: the first update of a pass
+        # goes to the GPU at once, and while a launch runs the host queues the next,
+        # twice as large one (a pass of 15 updates: 5 launches, not 15)
+        if len(self._queue) >= min(self._launch_at, max(1, self.defer_batches)):
+            self._launch_at *= 2
+            self._launch_queue()
+
+    def _launch_queue(self):
+        """Launch the queued updates: consecutive updates with the same job templates
+        and operand alignment become one multi-batch job per row-major factor
+        (channel-major / im2col jobs, already B*Ho*Wo rows of K each, stay one job
+        per batch)."""
+        queue, self._queue = self._queue, []
+        for _jobs, _ptrs, keep, versions, _dev, _key in queue:
+            for t, v in zip(keep, versions):
+                if t._version != v:
+                    raise RuntimeError(
+                        "a KFAC record was modified in place after update() and before its "
+                        "queued factor update ran; clone it, or set kfac.defer_batches = 1")
+        device = queue[0][4]
+        groups, start = [], 0
+        align = [tuple(p % 16 for p in e[1]) for e in queue]
+        for i in range(1, len(queue) + 1):
+            if i == len(queue) or queue[i][5] is not queue[start][5] or align[i] != align[start]:
+                groups.append(queue[start:i])
+                start = i
+        tables = []
+        for group in groups:
+            tmpl = group[0][0]
+            jobs = []
+            for k, t in enumerate(tmpl):
+                if len(group) > 1 and t.x.layout == N.ROWMAJOR:
+                    job = N.FactorJob.from_buffer_copy(t)
+                    job.x.ptr = group[0][1][k]
+                    table = N.segment_table([e[1][k] for e in group])
+                    tables.append(table)
+                    job.seg_ptrs, job.nseg = N.table_ptr(table), len(group)
+                    jobs.append(job)
+                else:
+                    for i, e in enumerate(group):
+                        job = N.FactorJob.from_buffer_copy(t)
+                        job.x.ptr = e[1][k]
+                        if i:
+                            job.beta = 1.0  # later batches add to the first one's result
+                        jobs.append(job)
             self._defer(jobs, device)
-        N.factor_update(jobs, device)
+            N.factor_update(jobs, device)
+        # queued records are released here (the host segment tables were read by the
+        # calls); the caching allocator orders any reuse of the records' memory after
+        # the launches on this stream
+        del tables, queue
 
     def _defer(self, jobs, device):
-        """Point each job at its accumulator: continue the pending cycle when it
-        targets the same factors, else (first update, or new targets) flush and plan
-        a new cycle for this batch shape."""
-        pending = self._acc_flush
-        if pending is not None and (device != self._acc_device or len(pending) != len(jobs)
-                                    or any(p.F != j.F for p, j in zip(pending, jobs))):
-            self.flush()
-            pending = None
-        if pending is not None:
-            for p, j in zip(pending, jobs):
-                j.acc, j.acc_splits, j.acc_beta = p.acc, p.acc_splits, 1.0
-            return
-        plan = N.factor_accum_plan(jobs)
-        offs, total = [], 0
-        for _splits, nbytes in plan:
-            offs.append(total)
-            total += (nbytes + 255) // 256 * 256
-        buf = self._acc_buf
-        if buf is None or buf.device != device or buf.numel() < total:
-            buf = self._acc_buf = torch.empty(total, dtype=torch.uint8, device=device)
-        base = buf.data_ptr()
-        flush = []
-        for j, (splits, _nbytes), off in zip(jobs, plan, offs):
-            j.acc, j.acc_splits, j.acc_beta = base + off, splits, 0.0
-            f = N.FactorJob.from_buffer_copy(j)
-            f.alpha = 1.0  # partials already carry alpha; f.beta: 0 fresh factor, 1 existing
-            flush.append(f)
-        self._acc_flush, self._acc_device = flush, device
+        """Point each job at its factor's accumulator: continue the pending cycle when
+        it already holds every target factor, else flush and plan a new cycle for this
+        launch's shapes (one accumulator per distinct factor)."""
+        if self._acc_map is not None and (device != self._acc_device or
+                                          any(j.F not in self._acc_map for j in jobs)):
+            acc_jobs, self._acc_flush, self._acc_map = self._acc_flush, None, None
+            N.factor_flush(acc_jobs, self._acc_device)
+        if self._acc_map is None:
+            first = {}
+            for j in jobs:
+                first.setdefault(j.F, j)
+            uniq = list(first.values())
+            plan = N.factor_accum_plan(uniq)
+            offs, total = [], 0
+            for _splits, nbytes in plan:
+                offs.append(total)
+                total += (nbytes + 255) // 256 * 256
+            buf = self._acc_buf
+            if buf is None or buf.device != device or buf.numel() < total:
+                buf = self._acc_buf = torch.empty(total, dtype=torch.uint8, device=device)
+            base = buf.data_ptr()
+            self._acc_map, self._acc_live, flush = {}, set(), []
+            for j, (splits, _nbytes), off in zip(uniq, plan, offs):
+                self._acc_map[j.F] = (base + off, splits)
+                f = N.FactorJob.from_buffer_copy(j)
+                f.seg_ptrs, f.nseg = None, 0
+                f.acc, f.acc_splits = base + off, splits
+                f.alpha = 1.0  # partials already carry alpha; f.beta: 0 fresh factor, 1 existing
+                flush.append(f)
+            self._acc_flush, self._acc_device = flush, device
+        for j in jobs:
+            j.acc, j.acc_splits = self._acc_map[j.F]
+            j.acc_beta = 1.0 if j.F in self._acc_live else 0.0
+            self._acc_live.add(j.F)
 
     # ------------------------------------------------------------------ invert
     def _damping(self, add, multiply):

@@ -82,6 +82,20 @@ typedef struct kfac_factor_job {
   float* acc;
   int32_t acc_splits;
   float acc_beta;
+  /* Optional multi-batch job (nseg > 1): the update covers nseg batches of x's
+   * shape at once, F += alpha * sum_s X_s~^T X_s~, X_s the operand x with
+   * ptr = seg_ptrs[s].  seg_ptrs is a HOST array of nseg device pointers, read
+   * during the call and passed to the kernel as launch arguments (no copy, no
+   * device table; graph-capturable); every base must share x.ptr's alignment
+   * modulo 16 bytes.  One launch then walks K across the batches in place
+   * (K = nseg * x.rows, up to 64 bases per launch, more run as back-to-back
+   * launches), so a pass of U equal batches costs about one MFMA launch instead
+   * of U.  Equivalent to nseg jobs with the same alpha (the reference's per-batch
+   * mean over equal batches).  nseg 0 or 1 = the single batch at x.ptr.  nseg > 1
+   * needs KFAC_ROWMAJOR (a Conv2d batch is already B*Ho*Wo rows of K).        */
+  const void* seg_ptrs;
+  int32_t nseg;
+  int32_t reserved2;
 } kfac_factor_job;
 
 /* Workspace (split-K slabs) needed by kfac_factor_update for these jobs. */

@@ -8,6 +8,9 @@ import ctypes
 import numpy as np
 
 
+UPDATES = []  # per kfac_factor_update call: nseg of each job
+
+
 def _view(ptr, count):
     return np.ctypeslib.as_array((ctypes.c_float * max(count, 1)).from_address(ptr))[:count]
 
@@ -16,12 +19,18 @@ def fake_factor_update(jobs, device):
     """kfac_factor_update: F = beta F + alpha X~^T X~, or with a deferred-reduction
     accumulator (modelled as one n x n split) acc = acc_beta acc + alpha X~^T X~."""
     from bnn_kfac_amd import _native as N
+    UPDATES.append([max(1, j.nseg) for j in jobs])
     for j in jobs:
         op = j.x
         assert op.layout == N.ROWMAJOR, "test double handles row-major operands only"
-        X = _view(op.ptr, op.rows * op.ld).reshape(op.rows, op.ld)[:, :op.cols].astype(np.float64)
+        if j.nseg > 1:  # multi-batch job: seg_ptrs is a (host) int64 table of batch bases
+            bases = np.ctypeslib.as_array((ctypes.c_int64 * j.nseg).from_address(j.seg_ptrs))
+        else:
+            bases = [op.ptr]
+        X = np.concatenate([_view(int(b), op.rows * op.ld).reshape(op.rows, op.ld)[:, :op.cols]
+                            for b in bases]).astype(np.float64)
         if op.has_ones:
-            X = np.concatenate([X, np.ones((op.rows, 1))], axis=1)
+            X = np.concatenate([X, np.ones((X.shape[0], 1))], axis=1)
         n = op.cols + op.has_ones
         if j.acc:
             assert j.acc_splits == 1

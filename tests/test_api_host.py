@@ -115,16 +115,18 @@ def test_deferred_reduce_host_logic(monkeypatch):
     rng = np.random.default_rng(3)
     batches = []
     for B in (8, 8, 5, 8):
-        batches.append([rng.random((B, 6), dtype=np.float32), rng.standard_normal((B, 5)).astype(np.float32),
-                        rng.random((B, 5), dtype=np.float32), rng.standard_normal((B, 3)).astype(np.float32)])
+        batches.append([torch.tensor(rng.random((B, 6), dtype=np.float32)),
+                        torch.tensor(rng.standard_normal((B, 5)).astype(np.float32)),
+                        torch.tensor(rng.random((B, 5), dtype=np.float32)),
+                        torch.tensor(rng.standard_normal((B, 3)).astype(np.float32))])
 
     def run(defer, read_after):
         net = mlp()
         kfac = KFAC(net)
         kfac.defer_reduce = defer
         for i, (a1, g1, a2, g2) in enumerate(batches):
-            kfac.record[net[0]] = [torch.from_numpy(a1), torch.from_numpy(g1)]
-            kfac.record[net[2]] = [torch.from_numpy(a2), torch.from_numpy(g2)]
+            kfac.record[net[0]] = [a1, g1]
+            kfac.record[net[2]] = [a2, g2]
             kfac.update(a1.shape[0])
             if i == read_after:
                 _ = kfac.state  # completes the pending reduction
@@ -141,6 +143,62 @@ def test_deferred_reduce_host_logic(monkeypatch):
     assert host_double.FLUSHES == [4, 4]  # read mid-pass, then the rest of the pass
     for g, w in zip(got, want):
         np.testing.assert_allclose(g, w, rtol=1e-6)
+
+
+def test_queued_updates_merge_into_multibatch_jobs(monkeypatch):
+    """update() queues; consecutive batches with matching operands become ONE
+    multi-batch job per factor (K walks every queued batch), a batch of another
+    shape starts a new group, `defer_batches` caps the queue, and the factors equal
+    the one-launch-per-update path."""
+    from bnn_kfac_amd.curvatures import KFAC
+    host_double.install(monkeypatch)
+    rng = np.random.default_rng(5)
+    sizes = (8, 8, 8, 5, 8, 8)
+    # torch.tensor copies into the CPU allocator's 64-byte-aligned blocks: equal
+    # base alignment, as device allocations have (batches merge only then)
+    batches = [[torch.tensor(rng.random((B, 6), dtype=np.float32)),
+                torch.tensor(rng.standard_normal((B, 5)).astype(np.float32)),
+                torch.tensor(rng.random((B, 5), dtype=np.float32)),
+                torch.tensor(rng.standard_normal((B, 3)).astype(np.float32))]
+               for B in sizes]
+
+    def run(defer_reduce, defer_batches=64):
+        host_double.UPDATES.clear()
+        net = mlp()
+        kfac = KFAC(net)
+        kfac.defer_reduce, kfac.defer_batches = defer_reduce, defer_batches
+        for a1, g1, a2, g2 in batches:
+            kfac.record[net[0]] = [a1, g1]
+            kfac.record[net[2]] = [a2, g2]
+            kfac.update(a1.shape[0])
+        factors = [t.clone().numpy() for pair in kfac.state.values() for t in pair]
+        return factors, [list(u) for u in host_double.UPDATES]
+
+    want, launches = run(False)
+    assert launches == [[1] * 4] * 6
+    got, launches = run(True)  # launch sizes 1, 2, 4: [8] [8 8 | 5] [8 8]
+    assert launches == [[1] * 4, [2] * 4, [1] * 4, [2] * 4]
+    for g, w in zip(got, want):
+        np.testing.assert_allclose(g, w, rtol=1e-6)
+    got, launches = run(True, defer_batches=2)  # [8] [8 8] [5 8] [8]
+    assert launches == [[1] * 4, [2] * 4, [1] * 4, [1] * 4, [1] * 4]
+    for g, w in zip(got, want):
+        np.testing.assert_allclose(g, w, rtol=1e-6)
+
+
+def test_queued_record_modified_in_place_raises(monkeypatch):
+    from bnn_kfac_amd.curvatures import KFAC
+    host_double.install(monkeypatch)
+    net = mlp()
+    kfac = KFAC(net)
+    for _ in range(2):  # the first update launches at once, the second is queued
+        a1 = torch.rand(4, 6)
+        kfac.record[net[0]] = [a1, torch.randn(4, 5)]
+        kfac.record[net[2]] = [torch.rand(4, 5), torch.randn(4, 3)]
+        kfac.update(4)
+    a1.mul_(2.0)
+    with pytest.raises(RuntimeError, match="modified in place"):
+        _ = kfac.state
 
 
 def test_save_load_roundtrip(tmp_path):

@@ -225,6 +225,78 @@ def test_deferred_reduce_raw_abi(hip_device):
     np.testing.assert_array_equal(F.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("cols,rows,offset,ones", [(784, 4096, 0, True), (128, 1000, 0, False),
+                                                    (129, 333, 0, True), (10, 4096, 0, False),
+                                                    (96, 777, 1, True), (31, 65, 0, True)])
+@pytest.mark.parametrize("deferred", [False, True])
+def test_multibatch_job_raw_abi(hip_device, cols, rows, offset, ones, deferred):
+    """One multi-batch job (nseg batches, each its own allocation, read in place
+    through the bases passed as kernel arguments) equals the sum over the batches, exactly on
+    small integers: LDS-DMA (aligned), register-staged (odd width / unaligned base)
+    and narrow (n <= 32) paths, ragged last stages, with and without accumulators."""
+    from bnn_kfac_amd import _native as N
+    rng = np.random.default_rng(cols + rows)
+    nseg = 5
+    xs = [rng.integers(-3, 4, size=(rows, cols)).astype(np.float32) for _ in range(nseg)]
+    # separate allocations; `offset` floats into each so every base has the same misalignment
+    bufs = [torch.empty(rows * cols + 8, device=hip_device) for _ in range(nseg)]
+    views = []
+    for b, x in zip(bufs, xs):
+        v = b[offset:offset + rows * cols].view(rows, cols)
+        v.copy_(_t(x, hip_device))
+        views.append(v)
+    n = cols + ones
+    F = torch.full((n, n), np.nan, device=hip_device)
+    table = N.segment_table([v.data_ptr() for v in views])
+    job = N.factor_job(N.rowmajor_operand(views[0], ones), F, 1.0, 0.0)
+    job.seg_ptrs, job.nseg = N.table_ptr(table), nseg
+    if deferred:
+        (splits, nbytes), = N.factor_accum_plan([job])
+        acc = torch.empty(nbytes, dtype=torch.uint8, device=hip_device)
+        job.acc, job.acc_splits, job.acc_beta = acc.data_ptr(), splits, 0.0
+        N.factor_update([job], hip_device)
+        f = N.factor_job(N.rowmajor_operand(views[0], ones), F, 1.0, 0.0)
+        f.acc, f.acc_splits = acc.data_ptr(), splits
+        N.factor_flush([f], hip_device)
+    else:
+        N.factor_update([job], hip_device)
+    want = np.zeros((n, n))
+    for x in xs:
+        xo = np.concatenate([x, np.ones((rows, 1), np.float32)], 1) if ones else x
+        want += xo.T.astype(np.float64) @ xo
+    np.testing.assert_array_equal(F.cpu().numpy(), want)
+
+
+def test_queued_pass_matches_per_batch_launches(hip_device):
+    """KFAC's default queued pass (multi-batch jobs, one short last batch, separate
+    record allocations) equals launching every update on its own."""
+    from bnn_kfac_amd.curvatures import KFAC
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Linear(784, 128), nn.ReLU(), nn.Linear(128, 10)).to(hip_device)
+    g = torch.Generator(device=hip_device).manual_seed(2)
+    recs = [(torch.rand(B, 784, device=hip_device, generator=g), torch.rand(B, 128, device=hip_device, generator=g),
+             torch.randn(B, 128, device=hip_device, generator=g), torch.randn(B, 10, device=hip_device, generator=g))
+            for B in (4096,) * 6 + (1700,)]
+    outs = []
+    for defer_batches in (1, 64, 4):
+        kfac = KFAC(net)
+        kfac.defer_batches = defer_batches
+        for a1, a2, g1, g2 in recs:
+            kfac.record[net[0]] = [a1, g1]
+            kfac.record[net[2]] = [a2, g2]
+            kfac.update(a1.shape[0])
+        outs.append([t.cpu().numpy() for pair in kfac.state.values() for t in pair])
+    for other in outs[1:]:
+        for got, want in zip(other, outs[0]):
+            np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-6 * np.abs(want).max())
+    ref = O.OracleKFAC(np.float64)
+    for a1, a2, g1, g2 in recs:
+        ref.update_linear("l0", a1.cpu().numpy(), g1.cpu().numpy(), True)
+        ref.update_linear("l1", a2.cpu().numpy(), g2.cpu().numpy(), True)
+    for got, want in zip(outs[1], [t for k in ("l0", "l1") for t in ref.state[k]]):
+        np.testing.assert_allclose(got, want, **FT)
+
+
 @pytest.mark.parametrize("model", ["mlp", "lenet"])
 def test_deferred_reduce_matches_immediate(hip_device, model):
     """KFAC.update with the deferred reduction (default) equals the per-update

@@ -1,2 +1,8 @@
 set -o pipefail
-timeout -k 10 300 python tools/host_overhead.py 2>&1 | grep "host issue" && timeout -k 10 600 python -m pytest tests -m gpu -x -q 2>&1 | tail -1 && timeout -k 10 300 python bench.py --no-cpu-baseline --no-e2e > gpurun_out/bench.log 2>&1; python -c "import json; d=json.loads(open('gpurun_out/bench.log').read().strip().splitlines()[-1]); print(round(d['value']/1e6,3), 'M img/s', round(d['ms_per_step'],3), 'ms', {k: round(v,4) for k,v in d['breakdown'].items()})"
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_factors.py -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_factors.log 2>&1; rc=$?
+tail -2 gpurun_out/gpu_factors.log; [ $rc -eq 0 ] || { grep -E "Error|assert|FAIL" gpurun_out/gpu_factors.log | head -20; exit $rc; }
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-e2e > gpurun_out/bench.log 2>&1 || exit $?
+python -c "import json; d=json.loads(open('gpurun_out/bench.log').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['roofline']['avg_launch_us'], d['roofline']['frac'], d['breakdown'])"
+timeout -k 10 300 python tools/host_overhead.py > gpurun_out/host.log 2>&1 || exit $?
+head -30 gpurun_out/host.log

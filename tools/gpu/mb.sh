@@ -1,2 +1,6 @@
 set -o pipefail
-cd tools/microbench && timeout -k 10 120 ./syrk_mb 1024 && timeout -k 10 120 ./syrk_mb 1024
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_factors.py -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_factors.log 2>&1; rc=$?
+tail -3 gpurun_out/gpu_factors.log; [ $rc -eq 0 ] || { grep -E "Error|assert|FAIL" gpurun_out/gpu_factors.log | head -20; exit $rc; }
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-e2e > gpurun_out/bench.log 2>&1 || exit $?
+python -c "import json; d=json.loads(open('gpurun_out/bench.log').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['roofline'], d['breakdown'])"

@@ -94,8 +94,7 @@ int main(int argc, char** argv) {
     int lt = 0; size_t off = 0;
     for (int i = 0; i < 4; ++i) {
       FactorJobDev& d = la.job[i];
-      d.x = to_dev(jobs[i].x); d.alpha = jobs[i].alpha; d.beta = 0; d.F = jobs[i].F; d.ldF = jobs[i].ldF;
-      d.n = factor_n(jobs[i]); d.t = (int)cdiv(d.n, TILE); d.splits = plans[i].splits; d.chunk = plans[i].chunk;
+      fill_dev(d, jobs[i]); d.beta = 0; d.splits = plans[i].splits; d.chunk = plans[i].chunk;
       d.slab = (float*)((char*)ws + off); off += plans[i].slab_bytes;
       d.task_begin = lt; d.tile_begin = 0; lt += plans[i].tiles * plans[i].splits; la.task_end[i] = lt;
     }
@@ -108,7 +107,6 @@ int main(int argc, char** argv) {
     la.stagger = 5;
     struct V { const char* name; TilesK k; } vs[] = {
         {"prod (BK32 x2 sched)", kfac_factor_tiles}, {"no stagger", kfac_factor_tiles_t<32, 2, 2 + 32>},
-        {"BK64 x2", kfac_factor_tiles_t<64, 2, 2>}, {"BK64 x2 nostag", kfac_factor_tiles_t<64, 2, 2 + 32>},
         {"32x4 sub2", kfac_factor_tiles_t<32, 4, 2, 2>}};
     for (auto& v : vs) {
       float t0 = time_tiles(v.k, la, lt, 50);
