@@ -10,8 +10,8 @@
 // reaches ~1e5 on the MLP).
 //
 // Blocked over 64x64 fp64 tiles; every launch is grouped over ALL factors:
-//   inv_build       R' = P R P (damped, symmetrised, identity padded); Z = 0
-//   inv_step(-1)    factor tile (0,0): X[0][0] = chol(R'[0][0])^{-1}
+//   inv_step(-1)    build R' = P R P (damped, symmetrised, identity padded), Z = 0,
+//                   info = 0; its workgroup 0 factors tile (0,0): X[0][0] = chol^{-1}
 //   for k = 0..T-1: inv_step(k), ONE launch per step, the panel folded in:
 //                   C_i = R'[i][k] X[k][k]^T formed where needed (never stored)
 //                   R'[i][j] -= C_i C_j^T                 (i >= j > k)
@@ -20,7 +20,9 @@
 //                   and the block owning (k+1,k+1) factors it right after its
 //                   update -> X[k+1][k+1] (one factorisation per step).
 //   [inv_xtx]       Y = X^T X (only for the full-inverse output)
-//   inv_out         L[i][j] = X[n-1-j][n-1-i]  (or R^{-1} = P Y P), fp32
+//   L[i][j] = X[n-1-j][n-1-i] (fp32) is written by the step that finalises each X
+//   tile (upper zero blocks by step -1): no separate output pass.  The full-inverse
+//   output (R^{-1} = P Y P) and the two-launch path (below) keep inv_out.
 // Z (the partially eliminated identity) lives in X's lower tiles.  Tile GEMMs
 // use v_mfma_f64_16x16x4_f64; the 64x64 diagonal factorisation is blocked by 16
 // (one wave eliminates each 16x16 diagonal block, MFMA for the rest).
@@ -51,6 +53,7 @@ struct InvJobDev {
   double scale, shift;
   int n, T, Np, kind;
   int xw;      // final strictly-lower X tiles in W (merged step) instead of X
+  int fout;    // merged step, inverse-Cholesky output: the steps write L (no inv_out)
 };
 
 struct InvArgs {
@@ -282,14 +285,11 @@ __device__ __forceinline__ void diag_factor(double* S, double* Y, double* dg) {
 
 // ------------------------------------------------------------------- build R'
 // R'[i][c] = scale*(F[fi][fc] + F[fc][fi])/2 + shift*[i==c], fi = n-1-i, fc = n-1-c.
-// Both source blocks are read row-coalesced into LDS (fp32), then combined.
-__global__ __launch_bounds__(NTHREADS) void inv_build(InvArgs args) {
-  __shared__ float P[NB * (NB + 1)];  // P[a][b] = F[fi(a)][fc(b)]
-  __shared__ float Q[NB * (NB + 1)];  // Q[b][a] = F[fc(b)][fi(a)]
-  const int j = find_job(args, blockIdx.x);
-  const InvJobDev& J = args.job[j];
-  int ti, tj;
-  tri_decode(blockIdx.x - args.begin[j], ti, tj);
+// Both source blocks are read row-coalesced into LDS (fp32, P and Q: 64 x 65 floats
+// each), then combined; tile (ti, tj) goes to W (and a copy to LDS `copy` when
+// non-null: the step -1 workgroup factors tile (0,0) straight from it).
+__device__ __forceinline__ void build_tile(const InvJobDev& J, int ti, int tj, float* P, float* Q,
+                                           double* copy) {
   const int n = J.n, i0 = ti * NB, c0 = tj * NB;
   constexpr int PER = NB * NB / NTHREADS;
   const int cc = threadIdx.x & 63, r0 = threadIdx.x >> 6;
@@ -320,8 +320,57 @@ __global__ __launch_bounds__(NTHREADS) void inv_build(InvArgs args) {
       v = (i == c) ? 1.0 : 0.0;  // identity padding keeps the padded block trivial
     }
     J.W[(int64_t)i * J.Np + c] = v;
+    if (copy) copy[a * DP + cc] = v;
     if (ti != tj) J.X[(int64_t)i * J.Np + c] = 0.0;  // Z accumulators start at 0
   }
+}
+
+// Output block of the final inverse tile X(a, b), a >= b, from LDS (pitch DP):
+// L[n-1-q][n-1-r] = X[r][q] (r in tile a, q in tile b).  Output rows are walked
+// with consecutive lanes on consecutive output columns (descending r): coalesced
+// stores.  zero = true writes the (all-zero) block of the upper tile X(b, a) instead.
+__device__ __forceinline__ void emit_out(const InvJobDev& J, int a, int b, const double* lds,
+                                         bool zero = false) {
+  const int n = J.n;
+  for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
+    const int cl = e >> 6, rl = NB - 1 - (e & 63);
+    const int r = a * NB + rl, q = b * NB + cl;
+    if (r >= n || q >= n) continue;
+    J.out[(int64_t)(n - 1 - q) * J.ldo + (n - 1 - r)] = zero ? 0.f : (float)lds[rl * DP + cl];
+  }
+}
+
+// Upper zero block of L for the strictly-lower tile (ti, tj): X(tj, ti) = 0, i.e.
+// L[n-1-q][n-1-r] = 0 for r in tile tj, q in tile ti.
+__device__ __forceinline__ void emit_zero_block(const InvJobDev& J, int ti, int tj) {
+  const int n = J.n;
+  for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
+    const int ql = e >> 6, rl = NB - 1 - (e & 63);
+    const int r = tj * NB + rl, q = ti * NB + ql;
+    if (r >= n || q >= n) continue;
+    J.out[(int64_t)(n - 1 - q) * J.ldo + (n - 1 - r)] = 0.f;
+  }
+}
+
+__global__ __launch_bounds__(NTHREADS) void inv_build(InvArgs args) {
+  __shared__ float P[NB * (NB + 1)];  // P[a][b] = F[fi(a)][fc(b)]
+  __shared__ float Q[NB * (NB + 1)];  // Q[b][a] = F[fc(b)][fi(a)]
+  const int j = find_job(args, blockIdx.x);
+  const InvJobDev& J = args.job[j];
+  const int local = blockIdx.x - args.begin[j];
+  if (local == 0 && threadIdx.x == 0 && J.info) *J.info = 0;
+  int ti, tj;
+  tri_decode(local, ti, tj);
+  build_tile(J, ti, tj, P, Q, nullptr);
+}
+
+// Pivot check of the factored diagonal tile d: info = first global column whose
+// pivot is not positive (+1), one ballot of wave 0 (no serial scan).
+__device__ __forceinline__ void check_pivots(const InvJobDev& J, int d, const double* dg) {
+  if (!J.info || threadIdx.x >= 64) return;
+  const int c = threadIdx.x, g = d * NB + c;
+  const unsigned long long bad = __ballot(g < J.n && !(dg[c] > 0.0));
+  if (bad && c == 0) atomicCAS(J.info, 0, d * NB + __ffsll(bad));
 }
 
 // acc (gemm64 layout) -> LDS tile
@@ -406,6 +455,7 @@ __device__ __forceinline__ void step_z(const InvJobDev& J, int k, int u, double*
   }
   gemm64<false>(S1, Bm, acc);
   store_acc_global(tile_ptr(J.X, J.Np, i, j), J.Np, acc, -1.0, true);
+  if (j < k && i == k + 1 && J.fout) emit_out(J, k, j, S2);  // final X[k][j]
 }
 
 // last row of X (k = T-1): X[k][j] = X[k][k] Z[k][j] -> W[k][j]
@@ -416,6 +466,12 @@ __device__ __forceinline__ void step_last_row(const InvJobDev& J, int k, int j, 
   doublex4 acc[4];
   gemm64<false>(S0, S1, acc);
   store_acc_global(tile_ptr(J.W, J.Np, k, j), J.Np, acc, 1.0, false);
+  if (J.fout) {
+    __syncthreads();  // S1 fully read by the GEMM
+    store_acc_lds(S1, acc);
+    __syncthreads();
+    emit_out(J, k, j, S1);
+  }
 }
 
 __global__ __launch_bounds__(NTHREADS) void inv_step(InvArgs args) {
@@ -428,8 +484,14 @@ __global__ __launch_bounds__(NTHREADS) void inv_step(InvArgs args) {
   const int k = args.step, T = J.T;
   const int local = blockIdx.x - args.begin[jb];
   const int nTrail = (T - k - 1) * (T - k) / 2;
-  if (k < 0) {  // first diagonal tile
-    load_tile(S2, tile_ptr(J.W, J.Np, 0, 0), J.Np);
+  if (k < 0) {  // build R' (one tile per workgroup); workgroup 0 also factors tile (0,0)
+    int ti, tj;
+    tri_decode(local, ti, tj);
+    if (local == 0 && threadIdx.x == 0 && J.info) *J.info = 0;
+    build_tile(J, ti, tj, reinterpret_cast<float*>(S0), reinterpret_cast<float*>(S1),
+               local == 0 ? S2 : nullptr);
+    if (J.fout && ti != tj) emit_zero_block(J, ti, tj);
+    if (local != 0) return;
     __syncthreads();
   } else if (k == T - 1) {
     step_last_row(J, k, local, S0, S1);
@@ -443,16 +505,9 @@ __global__ __launch_bounds__(NTHREADS) void inv_step(InvArgs args) {
   // the one diagonal factorisation of this step (single call site: stays inlined)
   const int d = k + 1;
   diag_factor(S2, S1, dg);
-  if (threadIdx.x == 0 && J.info) {
-    for (int c = 0; c < NB; ++c) {
-      const int g = d * NB + c;
-      if (g < J.n && !(dg[c] > 0.0)) {
-        atomicCAS(J.info, 0, g + 1);
-        break;
-      }
-    }
-  }
+  check_pivots(J, d, dg);
   store_tile(tile_ptr(J.X, J.Np, d, d), S1, J.Np);
+  if (J.fout) emit_out(J, d, d, S1);
 }
 
 // ------------------------------------------- two-launch step (large factors)
@@ -512,15 +567,7 @@ __global__ __launch_bounds__(NTHREADS) void inv_update(InvArgs args) {
       __syncthreads();
     }
     diag_factor(D, Yo, dg);
-    if (threadIdx.x == 0 && J.info) {
-      for (int c = 0; c < NB; ++c) {
-        const int g = i * NB + c;
-        if (g < J.n && !(dg[c] > 0.0)) {
-          atomicCAS(J.info, 0, g + 1);
-          break;
-        }
-      }
-    }
+    check_pivots(J, i, dg);
     store_tile(tile_ptr(J.X, J.Np, i, i), Yo, J.Np);
     return;
   }
@@ -669,24 +716,27 @@ static int invert_group(const kfac_invert_job* jobs, int njobs, char* ws, int32_
   }
   // latency-bound (few tiles per edge): one launch per step; else panel once per step
   const bool merged = Tmax <= MERGE_T;
-  for (int i = 0; i < njobs; ++i) args.job[i].xw = merged;
-  int rc;
-  if (info) {
-    if (hipMemsetAsync(info, 0, sizeof(int32_t) * njobs, s) != hipSuccess) return KFAC_ELAUNCH;
+  bool all_fused = merged;
+  for (int i = 0; i < njobs; ++i) {
+    args.job[i].xw = merged;
+    args.job[i].fout = merged && args.job[i].kind == KFAC_OUT_INV_CHOL;
+    all_fused &= args.job[i].fout != 0;
   }
-  rc = launch(inv_build, args, [](const InvJobDev& d) { return d.T * (d.T + 1) / 2; }, s);
-  if (rc) return rc;
+  int rc;
+  // info is zeroed by the first launch (workgroup 0 of each job)
   if (merged) {
     for (int k = -1; k < Tmax; ++k) {
       args.step = k;
       rc = launch(inv_step, args, [k](const InvJobDev& d) {
-        if (k < 0) return 1;
+        if (k < 0) return d.T * (d.T + 1) / 2;  // build every tile; workgroup 0 factors (0,0)
         if (k + 1 < d.T) return (d.T - k - 1) * (d.T - k) / 2 + (d.T - k - 1) * (k + 1);
         return k + 1 == d.T ? k : 0;  // last row of X
       }, s);
       if (rc) return rc;
     }
   } else {
+    rc = launch(inv_build, args, [](const InvJobDev& d) { return d.T * (d.T + 1) / 2; }, s);
+    if (rc) return rc;
     args.step = -1;
     rc = launch(inv_update, args, [](const InvJobDev&) { return 1; }, s);
     if (rc) return rc;
@@ -705,7 +755,8 @@ static int invert_group(const kfac_invert_job* jobs, int njobs, char* ws, int32_
                 [](const InvJobDev& d) { return d.kind == KFAC_OUT_INVERSE ? d.T * (d.T + 1) / 2 : 0; }, s);
     if (rc) return rc;
   }
-  return launch(inv_out, args, [](const InvJobDev& d) { return d.T * d.T; }, s);
+  if (all_fused) return KFAC_OK;  // the steps already wrote every L
+  return launch(inv_out, args, [](const InvJobDev& d) { return d.fout ? 0 : d.T * d.T; }, s);
 }
 
 }  // namespace kfac
