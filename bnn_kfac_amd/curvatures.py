@@ -69,6 +69,21 @@ class Curvature(ABC):
         self.flush()
         self._state = value
 
+    # `inv_state` reads first settle the verdict of a pending inversion (see
+    # KFAC.invert: the device's pivot check is read back asynchronously, so invert()
+    # does not stall the host on the GPU).  Writes never wait.
+    @property
+    def inv_state(self):
+        self._check_inverse()
+        return self._inv_state
+
+    @inv_state.setter
+    def inv_state(self, value):
+        self._inv_state = value
+
+    def _check_inverse(self):
+        pass
+
     def flush(self):
         """Complete deferred work so that `state` holds every update so far."""
 
@@ -170,6 +185,8 @@ class KFAC(Curvature):
         self._acc_live = set()   # F pointers already written in the pending cycle
         self._acc_flush = None   # flush jobs of the pending cycle (None: nothing pending)
         self._acc_device = None
+        self._info_host = None   # pinned int32 readback of the last inversion's pivot check
+        self._inv_pending = None  # (event, host info, layers, inv_state dict) until settled
 
     def reset(self):
         """Forget the accumulated factors (start a new data pass); device buffers are kept."""
@@ -468,7 +485,7 @@ class KFAC(Curvature):
     def invert(self, add: Union[float, list, tuple] = 0., multiply: Union[float, list, tuple] = 1.):
         """L = cholesky(inverse(sqrt(s) F + sqrt(n) I)) per factor (curvatures.py:367-398)."""
         assert self.state, "State dict is empty. Did you call 'update' prior to this?"
-        if self.inv_state:
+        if self.inv_state:  # (settles the previous inversion's verdict first)
             Warning("State has already been inverted. Is this expected?")
         damping = self._damping(add, multiply)
         jobs, outs = [], []
@@ -484,15 +501,40 @@ class KFAC(Curvature):
                 device = F_.device
             outs.append((layer, tuple(pair)))
         info = N.invert(jobs, device)
-        bad = info.cpu()
-        if bool((bad != 0).any()):
-            # The reference falls back to numpy (curvatures.py:393-396), which raises for
-            # a factor that is not positive definite; the fp64 device factorisation fails
-            # exactly there, so end the same way without a CPU path.
+        # The pivot verdict travels back with a non-blocking copy into pinned memory;
+        # it is settled (event wait) at the next read of `inv_state` or the next
+        # invert(), so a data pass can be queued behind this inversion without a
+        # host sync in between.
+        host = self._info_host
+        if host is None or host.numel() != info.numel():
+            host = self._info_host = torch.empty(info.numel(), dtype=info.dtype, pin_memory=True)
+        host.copy_(info, non_blocking=True)
+        done = torch.cuda.Event()
+        done.record(torch.cuda.current_stream(device))
+        for layer, pair in outs:
+            self._inv_state[layer] = pair
+        self._inv_pending = (done, host, [layer for layer, _ in outs], self._inv_state)
+
+    def _check_inverse(self):
+        """Settle a pending inversion: a factor that is not positive definite ends as
+        the reference's does (curvatures.py:393-396: torch fails, the numpy fallback
+        raises LinAlgError), the layers from the first failing one on dropped from
+        `inv_state` as the reference never assigns them."""
+        pending = getattr(self, "_inv_pending", None)
+        if pending is None:
+            return
+        self._inv_pending = None
+        done, host, layers, target = pending
+        done.synchronize()
+        bad = host.numpy()
+        if bad.any():
+            first = int(np.flatnonzero(bad)[0]) // 2  # two jobs (A, G) per layer
+            for layer in layers[first:]:
+                target.pop(layer, None)
+            # the fp64 device factorisation fails exactly where numpy's fallback
+            # would, so end the same way without a CPU path
             print("PyTorch Cholesky is singular. Using Numpy.")
             raise np.linalg.LinAlgError("Matrix is not positive definite")
-        for layer, pair in outs:
-            self.inv_state[layer] = pair
 
     # ------------------------------------------------------------------ sample
     def sample(self, layer: Module) -> Tensor:

@@ -118,8 +118,15 @@ def test_singular_raises_linalgerror(hip_device):
     kfac = KFAC(net)
     kfac.record[net[0]] = [_t(g["a"], hip_device), _t(g["g"], hip_device)]
     kfac.update(2)
+    kfac.invert(0.0, 1.0)  # the verdict is read back asynchronously ...
     with pytest.raises(np.linalg.LinAlgError):
-        kfac.invert(0.0, 1.0)
+        _ = kfac.inv_state  # ... and settled at the next inv_state read
+    assert net[0] not in kfac.inv_state
+    kfac.invert(0.0, 1.0)
+    with pytest.raises(np.linalg.LinAlgError):
+        kfac.invert(1.0, 1.0)  # or at the start of the next invert() (which then does not run)
+    kfac.invert(1.0, 1.0)
+    assert net[0] in kfac.inv_state
 
 
 def test_invert_identity_property_wide(hip_device):
