@@ -406,6 +406,263 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
 #define kfac_factor_tiles_channel kfac_factor_tiles_t<32, 2, 2, 1, KFAC_CHANNEL>
 #define kfac_factor_tiles_patch kfac_factor_tiles_t<32, 2, 2, 1, KFAC_PATCH>
 
+// ------------------------------------------------------------ conv operands
+// Conv2d factors with each image staged whole in LDS (replaces the per-element
+// register gather of the im2col / channel-major panel loaders for images that fit).
+// F = sum_rows P[row]^T P[row], row = (image b, output position):
+//   PATCH   (A, implicit F.unfold): P[(oh,ow)][(c,ki,kj)] = x_pad[b][c][oh*sh+ki][ow*sw+kj]
+//   CHANNEL (G, permute(1,0,2,3)):  P[pos][c] = g[b][c][pos]
+// A task is a tile (or the one narrow block) over WHOLE images.  Each image is
+// staged into LDS once (coalesced loads of the next image in flight meanwhile);
+// zero padding, the bias ones column and tile padding live in planes filled once
+// per task.  An MFMA's k-lanes take different output ROWS (PATCH: oh = g*KR + k;
+// CHANNEL: contiguous position segments), so along a row every lane's operand is
+// one LDS read at base_lane + t*stride: no per-MFMA index arithmetic (stride 1:
+// immediate offsets).  Rows past Ho read the A operand from the zero plane.
+//   n <= 16 : one 16x16 block, v_mfma_f32_16x16x4f32 (KR = 4), the 4 waves take
+//             different row groups / segments;
+//   n <= 32 : one 32x32 quadrant, 32x32x2 (KR = 2), split over waves the same way;
+//   else    : 64x64 tiles, one 32x32 quadrant per wave (diagonal tiles skip the
+//             strictly-upper one), as the row-major path.
+// Partials go to the task's slab / accumulator exactly as the other paths.
+constexpr int CONV_LDS_MAX = 12288;  // staged floats per workgroup (48 KB of LDS)
+constexpr int CONV_SRC_MAX = 2048;   // per-image staged elements (PATCH) / float4s (CHANNEL)
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+struct ConvGeom {
+  int mode;        // 0: 64x64 tiles, 1: narrow 32x32, 2: narrow 16x16
+  int KR;          // k-lanes per MFMA (2 or 4)
+  int B;           // images of the batch
+  int T;           // MFMAs along one row group (PATCH: Wo; CHANNEL: segment length Q)
+  int G;           // row groups (PATCH: ceil(Ho / KR)); CHANNEL: 1
+  int stride;      // LDS step between consecutive MFMAs (PATCH: sw; CHANNEL: 1)
+  int rowstep;     // PATCH: sh * Wp (one output row); CHANNEL: Q (one segment)
+  int Ho;          // PATCH: output rows
+  int plane;       // PATCH: Hp * Wp; CHANNEL: Lp = segments * Q (channel pitch)
+  int Wp;          // PATCH: padded row pitch
+  int ones_base;   // LDS offset of the all-ones plane (PATCH bias column)
+  int zero_base;   // LDS offset of the all-zero plane (tile padding, rows past Ho)
+  int lds;         // floats of LDS (>= the narrow reduce's 3 x 16 x 64)
+  int src;         // staged source elements (PATCH) / float4s (CHANNEL) per image
+};
+
+template <int LAYOUT, int PMAXE, bool STRIDE1>
+__global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args, ConvGeom cg) {
+  extern __shared__ __attribute__((aligned(16))) float cimg[];
+  const int task = xcd_task(blockIdx.x, gridDim.x);
+  int jx = 0;
+  while (jx + 1 < args.njobs && task >= args.task_end[jx]) ++jx;
+  const FactorJobDev& J = args.job[jx];
+  const OpDev& op = J.x;
+  const int local = task - J.task_begin;
+  const int tile = local / J.splits, split = local - tile * J.splits;
+  int ti, tj;
+  tri_decode(tile, ti, tj);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int mode = cg.mode;
+  const int klane = mode == 2 ? lane >> 4 : lane >> 5;
+  const int64_t b0 = (int64_t)split * cg.B / J.splits, b1 = (int64_t)(split + 1) * cg.B / J.splits;
+
+  // staging map: source element (PATCH) / float4 (CHANNEL) q of this thread -> LDS index
+  int dmap[PMAXE];
+#pragma unroll
+  for (int q = 0; q < PMAXE; ++q) {
+    const int e = tid + q * NTHREADS;
+    int d = -1;
+    if (e < cg.src) {
+      if (LAYOUT == KFAC_PATCH) {
+        const int hw = op.H * op.W, c = e / hw, r = e - c * hw, h = r / op.W, w = r - h * op.W;
+        d = c * cg.plane + (h + op.ph) * cg.Wp + (w + op.pw);
+      } else {
+        const int L4 = (int)op.L >> 2, c = e / L4;
+        d = (c * cg.plane >> 2) + (e - c * L4);
+      }
+    }
+    dmap[q] = d;
+  }
+  floatx4 pre[PMAXE];  // PATCH uses [0]
+  auto fetch = [&](int64_t b) {
+    const float* src = op.ptr + b * op.sB;
+#pragma unroll
+    for (int q = 0; q < PMAXE; ++q) {
+      if (dmap[q] < 0) continue;
+      if (LAYOUT == KFAC_PATCH) pre[q][0] = src[tid + q * NTHREADS];
+      else pre[q] = reinterpret_cast<const floatx4*>(src)[tid + q * NTHREADS];
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int q = 0; q < PMAXE; ++q) {
+      if (dmap[q] < 0) continue;
+      if (LAYOUT == KFAC_PATCH) cimg[dmap[q]] = pre[q][0];
+      else reinterpret_cast<floatx4*>(cimg)[dmap[q]] = pre[q];
+    }
+  };
+
+  // per-lane operand columns -> LDS offset of the column's plane position
+  auto column = [&](int col) -> int {
+    if (col >= op.cols) return (col == op.ones) ? cg.ones_base : cg.zero_base;
+    if (LAYOUT == KFAC_PATCH) {
+      const int kk = op.kh * op.kw, c = col / kk, r = col - c * kk, ki = r / op.kw;
+      return c * cg.plane + ki * cg.Wp + (r - ki * op.kw);
+    }
+    return col * cg.plane;
+  };
+  const int qi = mode ? 0 : wave >> 1, qj = mode ? 0 : wave & 1;
+  const bool same = ti == tj && qi == qj;
+  const bool active = mode ? true
+                           : !(ti == tj && qi < qj) && ti * TILE + qi * 32 < J.n &&
+                                 tj * TILE + qj * 32 < J.n;
+  const int cl = mode == 2 ? lane & 15 : lane & 31;
+  const int offA = column(ti * TILE + qi * 32 + cl);
+  const int offB = column(tj * TILE + qj * 32 + cl);
+
+  floatx16 acc32;
+  floatx4 acc16;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc32[v] = 0.f;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) acc16[v] = 0.f;
+
+  // one row group: T MFMAs, operands read two MFMAs ahead (LDS latency off the chain)
+  auto row_mfmas = [&](const float* pa, const float* pb, auto mfma) {
+    const int st = STRIDE1 ? 1 : cg.stride, T = cg.T, last = (T - 1) * st;
+    float a0 = pa[0], b0 = same ? a0 : pb[0];
+    float a1 = pa[min(st, last)], b1 = same ? a1 : pb[min(st, last)];
+    for (int t = 0; t < T; ++t) {
+      const int o = min((t + 2) * st, last);
+      const float a2 = pa[o], b2 = same ? a2 : pb[o];
+      mfma(a0, b0);
+      a0 = a1; b0 = b1;
+      a1 = a2; b1 = b2;
+    }
+  };
+  auto mfma16 = [&](float a, float b) { acc16 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc16, 0, 0, 0); };
+  auto mfma32 = [&](float a, float b) { acc32 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc32, 0, 0, 0); };
+  auto row = [&](const float* pa, const float* pb) {
+    if (mode == 2) row_mfmas(pa, pb, mfma16);
+    else row_mfmas(pa, pb, mfma32);
+  };
+
+  if (b0 < b1) fetch(b0);
+  // constant planes (and the zero padding / segment tails of the image planes)
+  for (int e = tid; e < cg.lds; e += NTHREADS)
+    cimg[e] = (LAYOUT == KFAC_PATCH && e >= cg.ones_base && e < cg.zero_base) ? 1.f : 0.f;
+  for (int64_t b = b0; b < b1; ++b) {
+    __syncthreads();  // every wave done with the previous image (and the fill)
+    commit();
+    __syncthreads();
+    if (b + 1 < b1) fetch(b + 1);  // next image's loads fly during the MFMAs
+    if (!active) continue;
+    if (LAYOUT == KFAC_PATCH) {
+      for (int g = mode ? wave : 0; g < cg.G; g += mode ? 4 : 1) {
+        const int oh = g * cg.KR + klane;
+        const int ra = oh < cg.Ho ? offA + oh * cg.rowstep : cg.zero_base;
+        const int rb = offB + min(oh, cg.Ho - 1) * cg.rowstep;
+        row(cimg + ra, cimg + rb);
+      }
+    } else {
+      const int sg = mode ? wave * cg.KR + klane : klane;
+      row(cimg + offA + sg * cg.rowstep, cimg + offB + sg * cg.rowstep);
+    }
+  }
+
+  float* out = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE;
+  if (mode == 1) {
+    store_narrow(J, out, acc32, cimg);
+    return;
+  }
+  if (mode == 2) {  // sum the 4 waves' 16x16 partials in wave order (deterministic)
+    __syncthreads();
+    if (wave > 0) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) cimg[((wave - 1) * 4 + v) * 64 + lane] = acc16[v];
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    // C/D map of 16x16x4: row = (lane >> 4) * 4 + v, col = lane & 15
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      float t = acc16[v];
+#pragma unroll
+      for (int w = 0; w < 3; ++w) t += cimg[(w * 4 + v) * 64 + lane];
+      float* at = &out[((lane >> 4) * 4 + v) * TILE + (lane & 15)];
+      if (!J.accum) *at = t;
+      else *at = J.sbeta == 0.f ? J.alpha * t : fmaf(J.sbeta, *at, J.alpha * t);
+    }
+    return;
+  }
+  if (!active) return;
+  out += qi * 32 * TILE + qj * 32;
+  put_partial(J, acc32, [&](int v) { return &out[acc_row(v, lane) * TILE + (lane & 31)]; });
+}
+
+// Geometry of a conv job on the LDS-staged kernel; false: the job takes the
+// register-staged path (images too large, channel blocks not float4-shaped, a
+// multi-batch job, or an empty batch).
+static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
+  const kfac_operand& o = j.x;
+  if ((o.layout != KFAC_PATCH && o.layout != KFAC_CHANNEL) || o.rows <= 0 || o.L <= 0 ||
+      j.nseg > 1 || o.rows % o.L != 0 || o.rows / o.L > (1 << 30))
+    return false;
+  const int n = o.cols + (o.has_ones ? 1 : 0);
+  g = ConvGeom{};
+  g.mode = n <= 16 ? 2 : (n <= 32 ? 1 : 0);
+  g.KR = g.mode == 2 ? 4 : 2;
+  g.B = (int)(o.rows / o.L);
+  int64_t lds;
+  if (o.layout == KFAC_PATCH) {
+    if ((int64_t)o.C * o.H * o.W > CONV_SRC_MAX) return false;
+    g.Wp = o.W + 2 * o.pw;
+    g.plane = (o.H + 2 * o.ph) * g.Wp;
+    g.Ho = o.Ho;
+    g.rowstep = o.sh * g.Wp;
+    g.T = o.Wo;
+    g.G = (int)cdiv(o.Ho, g.KR);
+    g.stride = o.sw;
+    g.ones_base = o.C * g.plane;
+    g.zero_base = g.ones_base + o.Ho * g.rowstep;
+    lds = (int64_t)g.zero_base + o.Ho * g.rowstep;
+    g.src = o.C * o.H * o.W;
+  } else {
+    const int64_t img = (int64_t)o.cols * o.L;
+    if (o.L % 4 != 0 || o.sB % 4 != 0 || reinterpret_cast<uintptr_t>(o.ptr) % 16 != 0 ||
+        img / 4 > CONV_SRC_MAX)
+      return false;
+    const int segs = g.mode ? 4 * g.KR : g.KR;  // narrow: the 4 waves' segments too
+    const int Q = (int)(cdiv(cdiv(o.L, segs), 4) * 4);
+    g.rowstep = Q;
+    g.plane = segs * Q;
+    g.T = Q;
+    g.G = 1;
+    g.stride = 1;
+    g.Ho = 1;
+    g.zero_base = g.ones_base = o.cols * g.plane;
+    lds = (int64_t)g.zero_base + g.plane;
+    g.src = (int)(img / 4);
+  }
+  lds = std::max<int64_t>(lds, 3 * 16 * 64);
+  if (lds > CONV_LDS_MAX) return false;
+  g.lds = (int)lds;
+  return true;
+}
+
+template <int LAYOUT>
+static void launch_conv(const FactorArgs& args, const ConvGeom& g, int tasks, hipStream_t stream) {
+  const size_t shmem = (size_t)g.lds * sizeof(float);
+  const bool s1 = g.stride == 1;
+  const int pm = (int)cdiv(g.src, NTHREADS);  // <= 8 by CONV_SRC_MAX
+#define KFAC_CONV_LAUNCH(PM, S1) \
+  hipLaunchKernelGGL((kfac_factor_conv<LAYOUT, PM, S1>), dim3(tasks), dim3(NTHREADS), shmem, stream, args, g)
+  if (pm <= 4) {
+    if (s1) KFAC_CONV_LAUNCH(4, true); else KFAC_CONV_LAUNCH(4, false);
+  } else {
+    if (s1) KFAC_CONV_LAUNCH(8, true); else KFAC_CONV_LAUNCH(8, false);
+  }
+#undef KFAC_CONV_LAUNCH
+}
+
 // One block = one 4-row strip of one 64x64 tile.  Each float4 of the strip is
 // summed by 4 threads over interleaved splits (part p: splits p, p+4, ...); the
 // partials combine in LDS in part order (deterministic; no atomics), then
@@ -540,6 +797,8 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
       continue;
     }
     p.splits = (int)cdiv(steps, best_c);
+    ConvGeom cg;
+    if (conv_geom(jobs[i], cg)) p.splits = std::min(p.splits, cg.B);  // tasks own whole images
     p.chunk = cdiv(steps, (int64_t)p.splits);
     p.slab_bytes = align_up((size_t)p.tiles * p.splits * TILE * TILE * sizeof(float), 256);
   }
@@ -632,12 +891,21 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
   {
     ProfScope ps(KFAC_PROF_FACTOR_TILES, stream);
     // launch_groups() gives every channel-major / im2col job a group of its own
+    // conv jobs whose images fit LDS: the image-staged kernel
+    ConvGeom cg;
+    const bool staged = njobs == 1 && conv_geom(jobs[0], cg);
     switch (jobs[0].x.layout) {
       case KFAC_CHANNEL:
-        hipLaunchKernelGGL(kfac_factor_tiles_channel, dim3(tasks), dim3(NTHREADS), 0, stream, args);
+        if (staged)
+          launch_conv<KFAC_CHANNEL>(args, cg, tasks, stream);
+        else
+          hipLaunchKernelGGL(kfac_factor_tiles_channel, dim3(tasks), dim3(NTHREADS), 0, stream, args);
         break;
       case KFAC_PATCH:
-        hipLaunchKernelGGL(kfac_factor_tiles_patch, dim3(tasks), dim3(NTHREADS), 0, stream, args);
+        if (staged)
+          launch_conv<KFAC_PATCH>(args, cg, tasks, stream);
+        else
+          hipLaunchKernelGGL(kfac_factor_tiles_patch, dim3(tasks), dim3(NTHREADS), 0, stream, args);
         break;
       default:
         hipLaunchKernelGGL(kfac_factor_tiles, dim3(tasks), dim3(NTHREADS), 0, stream, args);

@@ -127,6 +127,16 @@ def test_conv_golden(hip_device):
     (8, 5, 12, 12, 10, (5, 5), (1, 1), (0, 0), True),
     (3, 7, 9, 11, 70, (3, 2), (2, 3), (1, 0), False),
     (2, 13, 6, 6, 3, (1, 1), (1, 1), (0, 0), True),
+    # LDS-staged conv kernel: K splits inside images (B=64 / 256), 16x16 narrow im2col
+    # factor (n=10) with a 32-wide channel factor, 1x1 outputs (positions wrap every
+    # step), an im2col image too large to stage (register-staged fallback) next to a
+    # staged 8000-float gradient block, and a channel block not float4-sized (fallback)
+    (64, 6, 14, 14, 16, (5, 5), (1, 1), (0, 0), True),
+    (256, 1, 28, 28, 6, (5, 5), (1, 1), (2, 2), True),
+    (4, 1, 10, 10, 20, (3, 3), (1, 1), (1, 1), True),
+    (6, 3, 5, 5, 4, (5, 5), (1, 1), (0, 0), True),
+    (2, 3, 40, 40, 5, (3, 3), (1, 1), (1, 1), True),
+    (2, 2, 5, 5, 3, (3, 3), (1, 1), (0, 0), True),
 ])
 def test_conv_shapes_vs_oracle(hip_device, spec):
     from bnn_kfac_amd.curvatures import KFAC
