@@ -412,7 +412,7 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
 // F = sum_rows P[row]^T P[row], row = (image b, output position):
 //   PATCH   (A, implicit F.unfold): P[(oh,ow)][(c,ki,kj)] = x_pad[b][c][oh*sh+ki][ow*sw+kj]
 //   CHANNEL (G, permute(1,0,2,3)):  P[pos][c] = g[b][c][pos]
-// A task is a tile (or the one narrow block) over WHOLE images.  Each image is
+// A task is a group of blocks over WHOLE images.  Each image is
 // staged into LDS once (coalesced loads of the next image in flight meanwhile);
 // zero padding, the bias ones column and tile padding live in planes filled once
 // per task.  An MFMA's k-lanes take different output ROWS (PATCH: oh = g*KR + k;
@@ -422,13 +422,16 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
 //   n <= 16 : one 16x16 block, v_mfma_f32_16x16x4f32 (KR = 4), the 4 waves take
 //             different row groups / segments;
 //   n <= 32 : one 32x32 quadrant, 32x32x2 (KR = 2), split over waves the same way;
-//   else    : 64x64 tiles, one 32x32 quadrant per wave (diagonal tiles skip the
-//             strictly-upper one), as the row-major path.
-// Partials go to the task's slab / accumulator exactly as the other paths.
+//   else    : the lower triangle in 32x32 blocks, 4*CONV_CB per workgroup (CONV_CB
+//             per wave, balanced to one block; each image staged once for all).
+// Partials go to the slab / accumulator tiles exactly as the other paths (block
+// (bi, bj) = quadrant (bi & 1, bj & 1) of tile (bi / 2, bj / 2)).
 constexpr int CONV_LDS_MAX = 12288;  // staged floats per workgroup (48 KB of LDS)
 constexpr int CONV_SRC_MAX = 2048;   // per-image staged elements (PATCH) / float4s (CHANNEL)
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int CONV_CB = 2;  // 32x32 blocks per wave (mode 0): 4*CONV_CB per workgroup
 
 struct ConvGeom {
   int mode;        // 0: 64x64 tiles, 1: narrow 32x32, 2: narrow 16x16
@@ -445,9 +448,11 @@ struct ConvGeom {
   int zero_base;   // LDS offset of the all-zero plane (tile padding, rows past Ho)
   int lds;         // floats of LDS (>= the narrow reduce's 3 x 16 x 64)
   int src;         // staged source elements (PATCH) / float4s (CHANNEL) per image
+  int nq;          // mode 0: 32x32 blocks of the factor's lower triangle
+  int units;       // workgroups per K-split (mode 0: ceil(nq / (4*CONV_CB)) block groups; else 1)
 };
 
-template <int LAYOUT, int PMAXE, bool STRIDE1>
+template <int LAYOUT, int PMAXE, bool STRIDE1, int CB = CONV_CB>
 __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args, ConvGeom cg) {
   extern __shared__ __attribute__((aligned(16))) float cimg[];
   const int task = xcd_task(blockIdx.x, gridDim.x);
@@ -456,9 +461,7 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args,
   const FactorJobDev& J = args.job[jx];
   const OpDev& op = J.x;
   const int local = task - J.task_begin;
-  const int tile = local / J.splits, split = local - tile * J.splits;
-  int ti, tj;
-  tri_decode(tile, ti, tj);
+  const int unit = local / J.splits, split = local - unit * J.splits;  // unit: block group
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int mode = cg.mode;
   const int klane = mode == 2 ? lane >> 4 : lane >> 5;
@@ -509,40 +512,64 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args,
     }
     return col * cg.plane;
   };
-  const int qi = mode ? 0 : wave >> 1, qj = mode ? 0 : wave & 1;
-  const bool same = ti == tj && qi == qj;
-  const bool active = mode ? true
-                           : !(ti == tj && qi < qj) && ti * TILE + qi * 32 < J.n &&
-                                 tj * TILE + qj * 32 < J.n;
+  // Blocks of this wave.  mode 0: the factor's lower triangle in 32x32 blocks
+  // (b = tri index), 4*CB per workgroup (unit), block b = unit*4*CB + wave + 4i: the
+  // workgroup stages each image once for all its blocks and the waves' shares differ
+  // by at most one block.  Narrow modes: the one block, every wave.
   const int cl = mode == 2 ? lane & 15 : lane & 31;
-  const int offA = column(ti * TILE + qi * 32 + cl);
-  const int offB = column(tj * TILE + qj * 32 + cl);
+  int offA[CB], offB[CB], bij[CB];
+  bool same[CB];
+  int nmine = 0;
+#pragma unroll
+  for (int i = 0; i < CB; ++i) {
+    const int bidx = unit * 4 * CB + wave + 4 * i;
+    int bi = 0, bj = 0;
+    if (mode == 0) tri_decode(bidx, bi, bj);
+    const bool mine = mode ? i == 0 : bidx < cg.nq;
+    nmine += mine;
+    offA[i] = column(32 * bi + cl);
+    offB[i] = column(32 * bj + cl);
+    same[i] = bi == bj;
+    bij[i] = (bi << 16) | bj;
+  }
 
-  floatx16 acc32;
+  floatx16 acc[CB];
   floatx4 acc16;
 #pragma unroll
-  for (int v = 0; v < 16; ++v) acc32[v] = 0.f;
+  for (int i = 0; i < CB; ++i)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[i][v] = 0.f;
 #pragma unroll
   for (int v = 0; v < 4; ++v) acc16[v] = 0.f;
 
-  // one row group: T MFMAs, operands read two MFMAs ahead (LDS latency off the chain)
-  auto row_mfmas = [&](const float* pa, const float* pb, auto mfma) {
+  // one row group of one block: T MFMAs, operands read two MFMAs ahead (LDS latency
+  // off the accumulator chain)
+  auto row_mfmas = [&](const float* pa, const float* pb, bool sm, auto mfma) {
     const int st = STRIDE1 ? 1 : cg.stride, T = cg.T, last = (T - 1) * st;
-    float a0 = pa[0], b0 = same ? a0 : pb[0];
-    float a1 = pa[min(st, last)], b1 = same ? a1 : pb[min(st, last)];
+    float a0 = pa[0], b0 = sm ? a0 : pb[0];
+    float a1 = pa[min(st, last)], b1 = sm ? a1 : pb[min(st, last)];
     for (int t = 0; t < T; ++t) {
       const int o = min((t + 2) * st, last);
-      const float a2 = pa[o], b2 = same ? a2 : pb[o];
+      const float a2 = pa[o], b2 = sm ? a2 : pb[o];
       mfma(a0, b0);
       a0 = a1; b0 = b1;
       a1 = a2; b1 = b2;
     }
   };
-  auto mfma16 = [&](float a, float b) { acc16 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc16, 0, 0, 0); };
-  auto mfma32 = [&](float a, float b) { acc32 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc32, 0, 0, 0); };
-  auto row = [&](const float* pa, const float* pb) {
-    if (mode == 2) row_mfmas(pa, pb, mfma16);
-    else row_mfmas(pa, pb, mfma32);
+  // one row group of every block of this wave (rowA / rowB: LDS offsets added to the
+  // blocks' column offsets; zeroA: A read from the zero plane)
+  auto blocks = [&](int rowA, int rowB, bool zeroA) {
+    if (mode == 2) {
+      row_mfmas(cimg + (zeroA ? cg.zero_base : offA[0] + rowA), cimg + offB[0] + rowB, true,
+                [&](float a, float b) { acc16 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc16, 0, 0, 0); });
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      if (i >= nmine) break;
+      row_mfmas(cimg + (zeroA ? cg.zero_base : offA[i] + rowA), cimg + offB[i] + rowB, same[i],
+                [&](float a, float b) { acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i], 0, 0, 0); });
+    }
   };
 
   if (b0 < b1) fetch(b0);
@@ -554,23 +581,21 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args,
     commit();
     __syncthreads();
     if (b + 1 < b1) fetch(b + 1);  // next image's loads fly during the MFMAs
-    if (!active) continue;
+    if (nmine == 0) continue;
     if (LAYOUT == KFAC_PATCH) {
       for (int g = mode ? wave : 0; g < cg.G; g += mode ? 4 : 1) {
-        const int oh = g * cg.KR + klane;
-        const int ra = oh < cg.Ho ? offA + oh * cg.rowstep : cg.zero_base;
-        const int rb = offB + min(oh, cg.Ho - 1) * cg.rowstep;
-        row(cimg + ra, cimg + rb);
+        const int oh = g * cg.KR + klane;  // rows past Ho: A from the zero plane
+        blocks(oh * cg.rowstep, min(oh, cg.Ho - 1) * cg.rowstep, oh >= cg.Ho);
       }
     } else {
       const int sg = mode ? wave * cg.KR + klane : klane;
-      row(cimg + offA + sg * cg.rowstep, cimg + offB + sg * cg.rowstep);
+      blocks(sg * cg.rowstep, sg * cg.rowstep, false);
     }
   }
 
-  float* out = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE;
+  float* out = J.slab + (size_t)split * TILE * TILE;  // narrow: tile 0
   if (mode == 1) {
-    store_narrow(J, out, acc32, cimg);
+    store_narrow(J, out, acc[0], cimg);
     return;
   }
   if (mode == 2) {  // sum the 4 waves' 16x16 partials in wave order (deterministic)
@@ -593,9 +618,15 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args,
     }
     return;
   }
-  if (!active) return;
-  out += qi * 32 * TILE + qj * 32;
-  put_partial(J, acc32, [&](int v) { return &out[acc_row(v, lane) * TILE + (lane & 31)]; });
+  // block (bi, bj) = quadrant (bi & 1, bj & 1) of slab tile (bi / 2, bj / 2)
+#pragma unroll
+  for (int i = 0; i < CB; ++i) {
+    if (i >= nmine) break;
+    const int bi = bij[i] >> 16, bj = bij[i] & 0xffff, ti = bi >> 1, tj = bj >> 1;
+    float* o = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.splits + split) * TILE * TILE +
+               (bi & 1) * 32 * TILE + (bj & 1) * 32;
+    put_partial(J, acc[i], [&](int v) { return &o[acc_row(v, lane) * TILE + (lane & 31)]; });
+  }
 }
 
 // Geometry of a conv job on the LDS-staged kernel; false: the job takes the
@@ -644,6 +675,9 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
   }
   lds = std::max<int64_t>(lds, 3 * 16 * 64);
   if (lds > CONV_LDS_MAX) return false;
+  const int nb = (int)cdiv(n, 32);
+  g.nq = nb * (nb + 1) / 2;
+  g.units = g.mode ? 1 : (int)cdiv(g.nq, 4 * CONV_CB);
   g.lds = (int)lds;
   return true;
 }
@@ -741,6 +775,7 @@ __global__ __launch_bounds__(NTHREADS) void kfac_factor_reduce(FactorArgs args) 
 // ------------------------------------------------------------------- host side
 struct Plan {
   int tiles, splits;
+  int units;  // workgroups per K-split: tiles, or a staged conv job's block groups
   int64_t chunk;
   size_t slab_bytes;
 };
@@ -766,12 +801,15 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
   constexpr int64_t MIN_CHUNK = 8, OVERHEAD = 4;  // stages; ~per-task fixed cost in stages
   int64_t max_steps = 1;
   for (int i = 0; i < njobs; ++i) max_steps = std::max(max_steps, job_stages(jobs[i]));
+  int64_t units[MAXJ];
+  for (int i = 0; i < njobs; ++i) {
+    const int64_t t = cdiv(factor_n(jobs[i]), TILE);
+    ConvGeom cg;
+    units[i] = conv_geom(jobs[i], cg) ? cg.units : t * (t + 1) / 2;
+  }
   auto tasks_at = [&](int64_t c) {
     int64_t n = 0;
-    for (int i = 0; i < njobs; ++i) {
-      const int64_t t = cdiv(factor_n(jobs[i]), TILE);
-      n += t * (t + 1) / 2 * cdiv(job_stages(jobs[i]), c);
-    }
+    for (int i = 0; i < njobs; ++i) n += units[i] * cdiv(job_stages(jobs[i]), c);
     return n;
   };
   int64_t best_c = std::max(MIN_CHUNK, max_steps), best_cost = -1;
@@ -789,6 +827,7 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
     const int t = (int)cdiv(factor_n(jobs[i]), TILE);
     Plan& p = plans[i];
     p.tiles = t * (t + 1) / 2;
+    p.units = (int)units[i];
     const int64_t steps = job_stages(jobs[i]);
     if (jobs[i].acc) {
       p.splits = jobs[i].acc_splits;
@@ -883,7 +922,7 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
       red.tile_end[red.njobs++] = rtiles;
     }
     d.task_begin = tasks;
-    tasks += plans[i].tiles * plans[i].splits;
+    tasks += plans[i].units * plans[i].splits;
     args.task_end[i] = tasks;
   }
   if (off > ws_bytes) return KFAC_EWORKSPACE;
