@@ -73,6 +73,8 @@ SIGNATURES = {
     "kfac_invert_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(InvertJob), ctypes.c_int]),
     "kfac_invert": (ctypes.c_int, [ctypes.POINTER(InvertJob), ctypes.c_int, c_vp,
                                    ctypes.c_size_t, c_vp, c_vp]),
+    "kfac_invert_ex": (ctypes.c_int, [ctypes.POINTER(InvertJob), ctypes.c_int, c_vp,
+                                      ctypes.c_size_t, c_vp, c_vp, c_vp]),
     "kfac_damped_inv_chol": (ctypes.c_int, [c_vp, ctypes.c_int, c_i64, c_f64, c_f64, c_vp, c_i64,
                                             c_vp, ctypes.c_size_t, c_vp, c_vp]),
     "kfac_eig_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(EigJob), ctypes.c_int]),
@@ -201,16 +203,21 @@ def factor_flush(jobs, device: torch.device):
               "kfac_factor_flush")
 
 
-def invert(jobs, device: torch.device) -> torch.Tensor:
-    """Launch the grouped inversion; returns the DEVICE info tensor (int32, one per job)."""
+def invert(jobs, device: torch.device, inputs_read=None) -> torch.Tensor:
+    """Launch the grouped inversion on torch's current stream; returns the DEVICE info
+    tensor (int32, one per job).  `inputs_read` (a torch.cuda.Event, optional) is
+    recorded right after the launches that read the factors (kfac_invert_ex)."""
     L = lib()
     arr = as_array(InvertJob, jobs)
     need = L.kfac_invert_workspace_bytes(arr, len(jobs))
     stream = stream_handle(device)
     ws = workspace.get(device, need, stream)
     info = torch.empty(len(jobs), dtype=torch.int32, device=device)  # zeroed by kfac_invert
-    check(L.kfac_invert(arr, len(jobs), ws.data_ptr(), ws.numel(), info.data_ptr(), stream),
-          "kfac_invert")
+    ev = None
+    if inputs_read is not None:
+        ev = inputs_read.cuda_event
+    check(L.kfac_invert_ex(arr, len(jobs), ws.data_ptr(), ws.numel(), info.data_ptr(), ev, stream),
+          "kfac_invert_ex")
     return info
 
 

@@ -249,7 +249,11 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, const fl
   const int64_t s0 = (int64_t)split * J.chunk;
   const int64_t s1 = min(J.nst, s0 + J.chunk);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int qi = wave >> 1, qj = wave & 1;
+  // quadrant of this wave, rotated per dispatch round: the ~4 workgroups sharing a CU
+  // put their idle quadrants (strictly-upper on diagonal tiles, tile padding) on
+  // different SIMDs instead of all on the same one
+  const int qw = (MODE & 128) ? wave : (wave + (int)(blockIdx.x >> 8)) & 3;
+  const int qi = qw >> 1, qj = qw & 1;
   const bool same = ti == tj;
   const bool active = !(same && qi < qj) && ti * TILE + qi * 32 < J.n && tj * TILE + qj * 32 < J.n;
   const bool narrow = J.n <= 32;  // one 32x32 quadrant: the 4 waves split K instead

@@ -686,8 +686,10 @@ static int launch(void (*kern)(InvArgs), InvArgs& args, Count count, hipStream_t
   return KFAC_OK;
 }
 
+// Phase 0 = the launch that reads F (merged: step -1, which builds R' and factors
+// tile (0,0); two-launch path: inv_build); phase 1 = everything after it.
 static int invert_group(const kfac_invert_job* jobs, int njobs, char* ws, int32_t* info,
-                        hipStream_t s) {
+                        hipStream_t s, int phase) {
   InvArgs args{};
   args.njobs = njobs;
   int Tmax = 0;
@@ -725,7 +727,7 @@ static int invert_group(const kfac_invert_job* jobs, int njobs, char* ws, int32_
   int rc;
   // info is zeroed by the first launch (workgroup 0 of each job)
   if (merged) {
-    for (int k = -1; k < Tmax; ++k) {
+    for (int k = phase ? 0 : -1; k < (phase ? Tmax : 0); ++k) {
       args.step = k;
       rc = launch(inv_step, args, [k](const InvJobDev& d) {
         if (k < 0) return d.T * (d.T + 1) / 2;  // build every tile; workgroup 0 factors (0,0)
@@ -734,9 +736,9 @@ static int invert_group(const kfac_invert_job* jobs, int njobs, char* ws, int32_
       }, s);
       if (rc) return rc;
     }
+    if (!phase) return KFAC_OK;
   } else {
-    rc = launch(inv_build, args, [](const InvJobDev& d) { return d.T * (d.T + 1) / 2; }, s);
-    if (rc) return rc;
+    if (!phase) return launch(inv_build, args, [](const InvJobDev& d) { return d.T * (d.T + 1) / 2; }, s);
     args.step = -1;
     rc = launch(inv_update, args, [](const InvJobDev&) { return 1; }, s);
     if (rc) return rc;
@@ -763,19 +765,17 @@ static int invert_group(const kfac_invert_job* jobs, int njobs, char* ws, int32_
 
 using namespace kfac;
 
+// every job has its own region (the groups' F-reading launches all run first)
 extern "C" size_t kfac_invert_workspace_bytes(const kfac_invert_job* jobs, int njobs) {
   if (!jobs || njobs <= 0) return 0;
-  size_t best = 0;
-  for (int g = 0; g < njobs; g += IMAXJ) {
-    size_t tot = 0;
-    for (int i = g; i < std::min(njobs, g + IMAXJ); ++i) tot += job_ws(jobs[i]);
-    best = std::max(best, tot);
-  }
-  return best;
+  size_t tot = 0;
+  for (int i = 0; i < njobs; ++i) tot += job_ws(jobs[i]);
+  return tot;
 }
 
-extern "C" int kfac_invert(const kfac_invert_job* jobs, int njobs, void* workspace,
-                           size_t workspace_bytes, int32_t* info, kfac_stream_t stream) {
+extern "C" int kfac_invert_ex(const kfac_invert_job* jobs, int njobs, void* workspace,
+                              size_t workspace_bytes, int32_t* info, void* inputs_read,
+                              kfac_stream_t stream) {
   if (njobs <= 0 || !jobs) return KFAC_EINVAL;
   for (int i = 0; i < njobs; ++i) {
     const kfac_invert_job& j = jobs[i];
@@ -786,12 +786,26 @@ extern "C" int kfac_invert(const kfac_invert_job* jobs, int njobs, void* workspa
   }
   if (workspace_bytes < kfac_invert_workspace_bytes(jobs, njobs)) return KFAC_EWORKSPACE;
   ProfScope ps(KFAC_PROF_INVERT, (hipStream_t)stream);
-  for (int g = 0; g < njobs; g += IMAXJ) {
-    const int rc = invert_group(jobs + g, std::min(IMAXJ, njobs - g), (char*)workspace,
-                                info ? info + g : nullptr, (hipStream_t)stream);
-    if (rc) return rc;
+  // every group's F-reading launch first, then the event, then the rest
+  for (int phase = 0; phase < 2; ++phase) {
+    char* ws = (char*)workspace;
+    for (int g = 0; g < njobs; g += IMAXJ) {
+      const int ng = std::min(IMAXJ, njobs - g);
+      const int rc = invert_group(jobs + g, ng, ws, info ? info + g : nullptr, (hipStream_t)stream,
+                                  phase);
+      if (rc) return rc;
+      for (int i = g; i < g + ng; ++i) ws += job_ws(jobs[i]);
+    }
+    if (phase == 0 && inputs_read &&
+        hipEventRecord((hipEvent_t)inputs_read, (hipStream_t)stream) != hipSuccess)
+      return KFAC_ELAUNCH;
   }
   return KFAC_OK;
+}
+
+extern "C" int kfac_invert(const kfac_invert_job* jobs, int njobs, void* workspace,
+                           size_t workspace_bytes, int32_t* info, kfac_stream_t stream) {
+  return kfac_invert_ex(jobs, njobs, workspace, workspace_bytes, info, nullptr, stream);
 }
 
 extern "C" int kfac_damped_inv_chol(const float* F, int n, int64_t ldF, double sqrt_s, double sqrt_n,

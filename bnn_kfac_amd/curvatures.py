@@ -186,7 +186,10 @@ class KFAC(Curvature):
         self._acc_flush = None   # flush jobs of the pending cycle (None: nothing pending)
         self._acc_device = None
         self._info_host = None   # pinned int32 readback of the last inversion's pivot check
-        self._inv_pending = None  # (event, host info, layers, inv_state dict) until settled
+        self._inv_pending = None  # (event, host info, layers, inv_state dict, outputs, on side
+                                  # stream) until settled
+        self.overlap_invert = True  # invert() on a side stream (see invert)
+        self._inv_streams = {}    # device index -> side stream
 
     def reset(self):
         """Forget the accumulated factors (start a new data pass); device buffers are kept."""
@@ -488,32 +491,56 @@ class KFAC(Curvature):
         if self.inv_state:  # (settles the previous inversion's verdict first)
             Warning("State has already been inverted. Is this expected?")
         damping = self._damping(add, multiply)
-        jobs, outs = [], []
-        device = None
-        for (layer, value), (n, s) in zip(self.state.items(), damping):
-            first, second = value
-            pair = []
-            for F_ in (first, second):
-                N.require_device(F_, "state", layer)
-                out = torch.empty_like(F_, memory_format=torch.contiguous_format)
-                jobs.append(N.invert_job(F_, out, s ** 0.5, n ** 0.5))
-                pair.append(out)
-                device = F_.device
-            outs.append((layer, tuple(pair)))
-        info = N.invert(jobs, device)
-        # The pivot verdict travels back with a non-blocking copy into pinned memory;
-        # it is settled (event wait) at the next read of `inv_state` or the next
-        # invert(), so a data pass can be queued behind this inversion without a
-        # host sync in between.
-        host = self._info_host
-        if host is None or host.numel() != info.numel():
-            host = self._info_host = torch.empty(info.numel(), dtype=info.dtype, pin_memory=True)
-        host.copy_(info, non_blocking=True)
-        done = torch.cuda.Event()
-        done.record(torch.cuda.current_stream(device))
+        entries = list(self.state.items())
+        for layer, (first, second) in entries:
+            N.require_device(first, "state", layer)
+            N.require_device(second, "state", layer)
+        device = entries[0][1][0].device
+        # The inversion runs on a high-priority side stream (overlap_invert): its
+        # critical path is a chain of single-workgroup tile factorisations, so the
+        # next data pass's SYRK launches fill the rest of the chip meanwhile.  The
+        # side stream starts after the work that produced `state`; the caller's
+        # stream waits only until the factors have been READ (kfac_invert_ex's
+        # inputs_read event, after the first launch), so it may overwrite them.
+        main = torch.cuda.current_stream(device)
+        side = self._side_stream(device) if self.overlap_invert else main
+        read = None
+        if side is not main:
+            side.wait_stream(main)
+            read = torch.cuda.Event()
+            read.record(side)  # creates the event; kfac_invert_ex records it again
+        outs, jobs = [], []
+        with torch.cuda.stream(side):
+            for (layer, value), (n, s) in zip(entries, damping):
+                pair = []
+                for F_ in value:
+                    out = torch.empty_like(F_, memory_format=torch.contiguous_format)
+                    jobs.append(N.invert_job(F_, out, s ** 0.5, n ** 0.5))
+                    pair.append(out)
+                outs.append((layer, tuple(pair)))
+            info = N.invert(jobs, device, inputs_read=read)
+            # The pivot verdict travels back with a non-blocking copy into pinned
+            # memory; it is settled (event wait) at the next read of `inv_state` or the
+            # next invert(), so a data pass can be queued behind this inversion without
+            # a host sync in between.
+            host = self._info_host
+            if host is None or host.numel() != info.numel():
+                host = self._info_host = torch.empty(info.numel(), dtype=info.dtype, pin_memory=True)
+            host.copy_(info, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(side)
+        if read is not None:
+            main.wait_event(read)
         for layer, pair in outs:
             self._inv_state[layer] = pair
-        self._inv_pending = (done, host, [layer for layer, _ in outs], self._inv_state)
+        self._inv_pending = (done, host, [layer for layer, _ in outs], self._inv_state,
+                             [t for _, pair in outs for t in pair], side is not main)
+
+    def _side_stream(self, device):
+        s = self._inv_streams.get(device.index)
+        if s is None:
+            s = self._inv_streams[device.index] = torch.cuda.Stream(device=device, priority=-1)
+        return s
 
     def _check_inverse(self):
         """Settle a pending inversion: a factor that is not positive definite ends as
@@ -524,8 +551,15 @@ class KFAC(Curvature):
         if pending is None:
             return
         self._inv_pending = None
-        done, host, layers, target = pending
+        done, host, layers, target, outs, on_side = pending
         done.synchronize()
+        if on_side:
+            # later work on the reading stream sees the finished factors, and the
+            # allocator keeps their memory until that work has run
+            cur = torch.cuda.current_stream(outs[0].device)
+            cur.wait_event(done)
+            for t in outs:
+                t.record_stream(cur)
         bad = host.numpy()
         if bad.any():
             first = int(np.flatnonzero(bad)[0]) // 2  # two jobs (A, G) per layer

@@ -151,6 +151,14 @@ typedef struct kfac_invert_job {
 KFAC_API size_t kfac_invert_workspace_bytes(const kfac_invert_job* jobs, int njobs);
 KFAC_API int kfac_invert(const kfac_invert_job* jobs, int njobs, void* workspace, size_t workspace_bytes,
                 int32_t* info, kfac_stream_t stream);
+/* kfac_invert that also signals when the inputs are consumed: `inputs_read` (a
+ * hipEvent_t, may be NULL) is recorded on `stream` right after the launches that
+ * read the F factors (the first of each job group: R' is built from F there), so
+ * the caller may overwrite F (e.g. accumulate the next data pass) once the event
+ * completes while the rest of the inversion still runs.  Same results as
+ * kfac_invert.                                                               */
+KFAC_API int kfac_invert_ex(const kfac_invert_job* jobs, int njobs, void* workspace,
+                   size_t workspace_bytes, int32_t* info, void* inputs_read, kfac_stream_t stream);
 /* Single-factor convenience: KFAC.invert for one factor. */
 KFAC_API int kfac_damped_inv_chol(const float* F, int n, int64_t ldF, double sqrt_s, double sqrt_n,
                          float* L, int64_t ldL, void* workspace, size_t workspace_bytes,

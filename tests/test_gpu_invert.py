@@ -144,3 +144,47 @@ def test_invert_identity_property_wide(hip_device):
     Ld = L.cpu().numpy().astype(np.float64)
     E = Ld.T @ R @ Ld  # = I for the exact factor (L^T R L = I  <=>  L L^T = R^{-1})
     assert np.abs(E - np.eye(n)).max() < 1e-3
+
+
+def test_overlapped_inversion_matches_serial(hip_device):
+    """invert() runs on the side stream and the next pass is queued right behind it
+    (the bench's pattern: nothing read in between, so pass k+1's SYRK overlaps
+    inversion k and its flush overwrites the factors inversion k read).  Every
+    pass's L factors equal the serial path's bit for bit."""
+    from bnn_kfac_amd.curvatures import KFAC
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Linear(784, 128), nn.ReLU(), nn.Linear(128, 10)).to(hip_device)
+    g = torch.Generator(device=hip_device).manual_seed(3)
+    passes = [[(torch.rand(2048, 784, device=hip_device, generator=g),
+                torch.randn(2048, 128, device=hip_device, generator=g),
+                torch.rand(2048, 128, device=hip_device, generator=g),
+                torch.randn(2048, 10, device=hip_device, generator=g)) for _ in range(3)]
+              for _ in range(3)]
+
+    def run(overlap):
+        kfac = KFAC(net)
+        kfac.overlap_invert = overlap
+        kept = []
+        for batches in passes:
+            kfac.reset()
+            for a1, g1, a2, g2 in batches:
+                kfac.record[net[0]] = [a1, g1]
+                kfac.record[net[2]] = [a2, g2]
+                kfac.update(a1.shape[0])
+            kfac.invert(0.04, 200)
+            kept.append(dict(kfac._inv_state))  # no settle: the next pass overlaps
+        _ = kfac.inv_state
+        torch.cuda.synchronize()
+        return [[t.cpu().numpy() for pair in d.values() for t in pair] for d in kept]
+
+    serial, overlapped = run(False), run(True)
+    for got_pass, want_pass in zip(overlapped, serial):
+        for got, want in zip(got_pass, want_pass):
+            np.testing.assert_array_equal(got, want)
+    # and pass 0 is right in its own terms: L^T R L = I on the oracle's damped factor
+    ref = O.OracleKFAC(np.float64)
+    for a1, g1, a2, g2 in passes[0]:
+        ref.update_linear("l0", a1.cpu().numpy(), g1.cpu().numpy(), True)
+    R = O.damped_factor(ref.state["l0"][0], 0.04, 200)
+    L = serial[0][0].astype(np.float64)
+    assert np.abs(L.T @ R @ L - np.eye(R.shape[0])).max() < 1e-3
