@@ -84,6 +84,10 @@ SIGNATURES = {
                                                         c_i64]),
     "kfac_kron_quadform": (ctypes.c_int, [ctypes.POINTER(QuadJob), ctypes.c_int, c_i64,
                                           ctypes.c_int, c_vp, c_vp, ctypes.c_size_t, c_vp]),
+    "kfac_cu_count": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+    "kfac_stream_create_cu_mask": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
+                                                  ctypes.POINTER(c_vp)]),
+    "kfac_stream_destroy": (ctypes.c_int, [c_vp]),
     "kfac_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "kfac_profile_read": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_int64)]),
@@ -219,6 +223,27 @@ def invert(jobs, device: torch.device, inputs_read=None) -> torch.Tensor:
     check(L.kfac_invert_ex(arr, len(jobs), ws.data_ptr(), ws.numel(), info.data_ptr(), ev, stream),
           "kfac_invert_ex")
     return info
+
+
+def cu_count(device: torch.device) -> int:
+    n = ctypes.c_int()
+    check(lib().kfac_cu_count(device.index if device.index is not None else 0, ctypes.byref(n)),
+          "kfac_cu_count")
+    return n.value
+
+
+def cu_mask_stream(device: torch.device, cus) -> "torch.cuda.ExternalStream":
+    """A stream confined to the CUs in `cus` (kfac_stream_create_cu_mask), as a torch
+    ExternalStream (the library keeps it for the process lifetime)."""
+    words = (max(cus) // 32 + 1) if cus else 1
+    mask = (ctypes.c_uint32 * words)()
+    for c in cus:
+        mask[c // 32] |= 1 << (c % 32)
+    handle = c_vp()
+    with torch.cuda.device(device):
+        check(lib().kfac_stream_create_cu_mask(mask, words, ctypes.byref(handle)),
+              "kfac_stream_create_cu_mask")
+    return torch.cuda.ExternalStream(handle.value, device=device)
 
 
 def syev(jobs, device: torch.device) -> torch.Tensor:

@@ -217,6 +217,16 @@ KFAC_API int kfac_profile_enable(int on);
 KFAC_API int kfac_profile_read(int id, double* total_ms, int64_t* launches);
 KFAC_API int kfac_profile_reset(void);
 
+/* ------------------------------------------------------------ CU partitions
+ * Streams whose dispatches are confined to a subset of the device's CUs
+ * (hipExtStreamCreateWithCUMask; bit i of mask word i/32 = CU i).  KFAC runs a
+ * data pass's SYRK launches and the (latency-bound, one-workgroup critical path)
+ * inversion of the previous pass on disjoint CU sets, so neither waits for the
+ * other's workgroups to drain from a CU.  kfac_cu_count: the device's CUs.   */
+KFAC_API int kfac_cu_count(int device, int* count);
+KFAC_API int kfac_stream_create_cu_mask(const uint32_t* mask, int words, void** stream);
+KFAC_API int kfac_stream_destroy(void* stream);
+
 /* ------------------------------------------------------------------- misc */
 KFAC_API const char* kfac_strerror(int status);
 KFAC_API const char* kfac_version(void);
