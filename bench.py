@@ -149,6 +149,8 @@ def main():
     ap.add_argument("--images", type=int, default=60000, help="images per rank per pass")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--partition", type=int, default=32,
+                    help="CUs reserved for the overlapped inversion (KFAC.partition_cus; 0 = none)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -158,6 +160,9 @@ def main():
     device = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
+    # all GPU work on one non-default stream (the legacy default stream would
+    # serialise with the CU-masked streams of --partition)
+    torch.cuda.set_stream(torch.cuda.Stream(device))
 
     from bnn_kfac_amd import _native as N
     from bnn_kfac_amd.curvatures import KFAC
@@ -167,6 +172,7 @@ def main():
     net = build_model(args.config, device)
     layers = [m for m in net.modules() if isinstance(m, (torch.nn.Linear, torch.nn.Conv2d))]
     kfac = DistributedKFAC(net) if world > 1 else KFAC(net)
+    kfac.partition_cus = args.partition
     recs = synthetic_records(specs, args.images, device, seed=1234 + rank)
     starts = list(range(0, args.images, args.batch))
 
@@ -270,7 +276,7 @@ def main():
                "config": {"workload": f"{NAMES[args.config]} KFAC factor pass over {args.images} "
                                       f"images/rank (batch {args.batch}/rank) + invert{DAMPING}",
                           "global_batch": args.batch * world, "images_per_rank": args.images,
-                          "parallelism": f"dp{world}"},
+                          "parallelism": f"dp{world}", "inversion_cus": args.partition or "shared"},
                "roofline": roofline, "cpu_baseline": cpu, "breakdown": breakdown,
                "e2e_images_per_s": e2e}
         print(json.dumps(out), flush=True)

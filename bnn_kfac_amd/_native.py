@@ -85,6 +85,7 @@ SIGNATURES = {
     "kfac_kron_quadform": (ctypes.c_int, [ctypes.POINTER(QuadJob), ctypes.c_int, c_i64,
                                           ctypes.c_int, c_vp, c_vp, ctypes.c_size_t, c_vp]),
     "kfac_cu_count": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+    "kfac_set_cu_budget": (ctypes.c_int, [ctypes.c_int]),
     "kfac_stream_create_cu_mask": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
                                                   ctypes.POINTER(c_vp)]),
     "kfac_stream_destroy": (ctypes.c_int, [c_vp]),
@@ -230,6 +231,11 @@ def cu_count(device: torch.device) -> int:
     check(lib().kfac_cu_count(device.index if device.index is not None else 0, ctypes.byref(n)),
           "kfac_cu_count")
     return n.value
+
+
+def set_cu_budget(cus: int) -> None:
+    """CUs the factor launches are planned for (kfac_set_cu_budget; 0 = all)."""
+    check(lib().kfac_set_cu_budget(int(cus)), "kfac_set_cu_budget")
 
 
 def cu_mask_stream(device: torch.device, cus) -> "torch.cuda.ExternalStream":

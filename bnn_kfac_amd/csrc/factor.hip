@@ -800,8 +800,13 @@ static int64_t job_stages(const kfac_factor_job& j) { return job_sps(j) * job_ns
 // A job with a deferred-reduction accumulator keeps the accumulator's split count
 // (its layout): its stage range is cut into that many equal chunks (trailing splits
 // of a smaller batch may be empty and then contribute zero).
+// CUs the SYRK launches may occupy (kfac_set_cu_budget): 0 = all 256.  Set when
+// part of the chip is reserved (a CU-masked inversion stream running beside them).
+static int g_cu_budget = 0;
+
 static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
-                      int64_t slots = 1024) {
+                      int64_t slots = 0) {
+  if (slots <= 0) slots = 4 * (int64_t)(g_cu_budget > 0 ? g_cu_budget : 256);
   constexpr int64_t MIN_CHUNK = 8, OVERHEAD = 4;  // stages; ~per-task fixed cost in stages
   int64_t max_steps = 1;
   for (int i = 0; i < njobs; ++i) max_steps = std::max(max_steps, job_stages(jobs[i]));
@@ -996,6 +1001,12 @@ static void launch_groups(const kfac_factor_job* jobs, int njobs, std::vector<kf
       sorted.push_back(jobs[i]);
       order.push_back(i);
     }
+}
+
+extern "C" int kfac_set_cu_budget(int cus) {
+  if (cus < 0 || cus > 4096) return KFAC_EINVAL;
+  g_cu_budget = cus;
+  return KFAC_OK;
 }
 
 extern "C" size_t kfac_factor_workspace_bytes(const kfac_factor_job* jobs, int njobs) {

@@ -43,6 +43,7 @@ typedef double doublex4 __attribute__((ext_vector_type(4)));
 
 struct InvJobDev {
   const float* F;
+  unsigned* cnt;  // inv_flow dependency counters (verR[T*T], verZ[T*T], diag[T]) or null
   int64_t ldF;
   float* out;
   int64_t ldo;
@@ -57,6 +58,7 @@ struct InvJobDev {
 };
 
 struct InvArgs {
+  unsigned* flow;  // inv_flow queue header {head, abort} (zeroed by the build step) or null
   int njobs;
   int step;
   int begin[IMAXJ + 1];
@@ -73,20 +75,45 @@ __device__ __forceinline__ double* tile_ptr(double* base, int Np, int ti, int tj
   return base + ((int64_t)ti * NB) * Np + (int64_t)tj * NB;
 }
 
+// Global access to the W / X workspace tiles.  C = true (inv_flow: tiles handed
+// between workgroups of ONE launch) uses the write-through form of the MI355X
+// hand-off recipe: every store `sc1` (global_store ... sc1, the line leaves the
+// XCD's L2), every load `sc1` (bypasses this CU's L1), so no release/acquire
+// fence is needed around the dependency counters.  C = false: plain accesses
+// (tiles cross kernel boundaries only).
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) unsigned gunsigned;
+template <bool C>
+__device__ __forceinline__ double gld(const double* p) {
+  if constexpr (C)
+    return __hip_atomic_load((gdouble*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    return *p;
+}
+template <bool C>
+__device__ __forceinline__ void gst(double* p, double v) {
+  if constexpr (C)
+    __hip_atomic_store((gdouble*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+
 // All 16 loads of a thread are issued before the first LDS write (a rolled loop
 // would serialise 16 global-memory round trips).
+template <bool C = false>
 __device__ __forceinline__ void load_tile(double* lds, const double* g, int Np) {
   constexpr int PER = NB * NB / NTHREADS;
   const int c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
   double v[PER];
 #pragma unroll
-  for (int q = 0; q < PER; ++q) v[q] = g[(int64_t)(r0 + 4 * q) * Np + c];
+  for (int q = 0; q < PER; ++q) v[q] = gld<C>(g + (int64_t)(r0 + 4 * q) * Np + c);
 #pragma unroll
   for (int q = 0; q < PER; ++q) lds[(r0 + 4 * q) * DP + c] = v[q];
 }
 
 // Up to three tiles with every load in flight together (one memory round trip
 // instead of one per tile); null destinations are skipped.
+template <bool C = false>
 __device__ __forceinline__ void load_tiles(double* l0, const double* g0, double* l1, const double* g1,
                                            double* l2, const double* g2, int Np) {
   constexpr int PER = NB * NB / NTHREADS;
@@ -95,9 +122,9 @@ __device__ __forceinline__ void load_tiles(double* l0, const double* g0, double*
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     const int64_t off = (int64_t)(r0 + 4 * q) * Np + c;
-    v0[q] = g0[off];
-    if (l1) v1[q] = g1[off];
-    if (l2) v2[q] = g2[off];
+    v0[q] = gld<C>(g0 + off);
+    if (l1) v1[q] = gld<C>(g1 + off);
+    if (l2) v2[q] = gld<C>(g2 + off);
   }
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
@@ -108,10 +135,11 @@ __device__ __forceinline__ void load_tiles(double* l0, const double* g0, double*
   }
 }
 
+template <bool C = false>
 __device__ __forceinline__ void store_tile(double* g, const double* lds, int Np) {
   for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) {
     const int r = e >> 6, c = e & 63;
-    g[(int64_t)r * Np + c] = lds[r * DP + c];
+    gst<C>(g + (int64_t)r * Np + c, lds[r * DP + c]);
   }
 }
 
@@ -149,16 +177,22 @@ __device__ __forceinline__ void gemm64(const double* A, const double* B, doublex
 }
 
 // global[tile](r, c) = alpha * acc (+ global if accumulate)   (acc from gemm64)
+template <bool C = false>
 __device__ __forceinline__ void store_acc_global(double* g, int Np, const doublex4 (&acc)[4],
                                                  double alpha, bool accumulate) {
   const int w = threadIdx.x >> 6, col = threadIdx.x & 15;
+  auto at = [&](int jb, int v) { return g + (int64_t)(16 * w + acc_row64(v)) * Np + 16 * jb + col; };
+  // every old value loaded before the first store: atomic (C) accesses keep program
+  // order, so an interleaved load/store per element would serialise 16 round trips
+  double old[4][4];
 #pragma unroll
   for (int jb = 0; jb < 4; ++jb)
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      double* p = g + (int64_t)(16 * w + acc_row64(v)) * Np + 16 * jb + col;
-      *p = accumulate ? *p + alpha * acc[jb][v] : alpha * acc[jb][v];
-    }
+    for (int v = 0; v < 4; ++v) old[jb][v] = accumulate ? gld<C>(at(jb, v)) : 0.0;
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) gst<C>(at(jb, v), old[jb][v] + alpha * acc[jb][v]);
 }
 
 // 1/d: v_rcp_f64 + two Newton steps (~1 ulp) instead of the IEEE division sequence,
@@ -406,22 +440,20 @@ __device__ __forceinline__ void panel_tile_lds(double* Sdst, const double* Xkk) 
 // Final inverse X: diagonal tiles in X, strictly-lower tiles in W (x_tile()).
 // trailing tile (i, j), i >= j > k: R'[i][j] -= C_i C_j^T.  Returns true for the
 // (k+1, k+1) workgroup, which then holds the updated diagonal tile in S0.
-__device__ __forceinline__ bool step_trailing(const InvJobDev& J, int k, int local, double* S0,
-                                              double* S1, double* S2) {
-  int a, b;
-  tri_decode(local, a, b);
-  const int i = k + 1 + a, j = k + 1 + b;
+template <bool C = false>
+__device__ __forceinline__ bool step_trailing_ij(const InvJobDev& J, int k, int i, int j, double* S0,
+                                                 double* S1, double* S2) {
   const bool diag = i == k + 1 && j == k + 1;
   // the (k+1,k+1) workgroup also prefetches its diagonal tile into the idle S2
-  load_tiles(S0, tile_ptr(J.X, J.Np, k, k), S1, tile_ptr(J.W, J.Np, i, k),
-             (j != i || diag) ? S2 : nullptr, tile_ptr(J.W, J.Np, j != i ? j : i, j != i ? k : i), J.Np);
+  load_tiles<C>(S0, tile_ptr(J.X, J.Np, k, k), S1, tile_ptr(J.W, J.Np, i, k),
+                (j != i || diag) ? S2 : nullptr, tile_ptr(J.W, J.Np, j != i ? j : i, j != i ? k : i), J.Np);
   __syncthreads();
   panel_tile_lds(S1, S0);              // C_i
   if (j != i) panel_tile_lds(S2, S0);  // C_j
   doublex4 acc[4];
   gemm64<true>(S1, j != i ? S2 : S1, acc);
   if (!diag) {
-    store_acc_global(tile_ptr(J.W, J.Np, i, j), J.Np, acc, -1.0, true);
+    store_acc_global<C>(tile_ptr(J.W, J.Np, i, j), J.Np, acc, -1.0, true);
     return false;
   }
   // the updated diagonal tile is consumed right here (never written back)
@@ -434,12 +466,20 @@ __device__ __forceinline__ bool step_trailing(const InvJobDev& J, int k, int loc
   return true;
 }
 
+template <bool C = false>
+__device__ __forceinline__ bool step_trailing(const InvJobDev& J, int k, int local, double* S0,
+                                              double* S1, double* S2) {
+  int a, b;
+  tri_decode(local, a, b);
+  return step_trailing_ij<C>(J, k, k + 1 + a, k + 1 + b, S0, S1, S2);
+}
+
 // Z tile (i, j), i > k >= j: Z[i][j] -= C_i B, B = X[k][k] (j = k) or
 // X[k][k] Z[k][j] (j < k; row k+1's workgroup also stores it as the final X[k][j]).
-__device__ __forceinline__ void step_z(const InvJobDev& J, int k, int u, double* S0, double* S1,
-                                       double* S2) {
-  const int i = k + 1 + u / (k + 1), j = u % (k + 1);
-  load_tiles(S0, tile_ptr(J.X, J.Np, k, k), S1, tile_ptr(J.W, J.Np, i, k), j < k ? S2 : nullptr,
+template <bool C = false>
+__device__ __forceinline__ void step_z_ij(const InvJobDev& J, int k, int i, int j, double* S0,
+                                          double* S1, double* S2) {
+  load_tiles<C>(S0, tile_ptr(J.X, J.Np, k, k), S1, tile_ptr(J.W, J.Np, i, k), j < k ? S2 : nullptr,
              tile_ptr(J.X, J.Np, k, j), J.Np);
   __syncthreads();
   panel_tile_lds(S1, S0);  // C_i
@@ -449,23 +489,30 @@ __device__ __forceinline__ void step_z(const InvJobDev& J, int k, int u, double*
     gemm64<false>(S0, S2, acc);
     __syncthreads();
     store_acc_lds(S2, acc);
-    if (i == k + 1) store_acc_global(tile_ptr(J.W, J.Np, k, j), J.Np, acc, 1.0, false);
+    if (i == k + 1 && J.xw) store_acc_global<C>(tile_ptr(J.W, J.Np, k, j), J.Np, acc, 1.0, false);
     __syncthreads();
     Bm = S2;
   }
   gemm64<false>(S1, Bm, acc);
-  store_acc_global(tile_ptr(J.X, J.Np, i, j), J.Np, acc, -1.0, true);
+  store_acc_global<C>(tile_ptr(J.X, J.Np, i, j), J.Np, acc, -1.0, true);
   if (j < k && i == k + 1 && J.fout) emit_out(J, k, j, S2);  // final X[k][j]
 }
 
+template <bool C = false>
+__device__ __forceinline__ void step_z(const InvJobDev& J, int k, int u, double* S0, double* S1,
+                                       double* S2) {
+  step_z_ij<C>(J, k, k + 1 + u / (k + 1), u % (k + 1), S0, S1, S2);
+}
+
 // last row of X (k = T-1): X[k][j] = X[k][k] Z[k][j] -> W[k][j]
+template <bool C = false>
 __device__ __forceinline__ void step_last_row(const InvJobDev& J, int k, int j, double* S0,
                                               double* S1) {
-  load_tiles(S0, tile_ptr(J.X, J.Np, k, k), S1, tile_ptr(J.X, J.Np, k, j), nullptr, nullptr, J.Np);
+  load_tiles<C>(S0, tile_ptr(J.X, J.Np, k, k), S1, tile_ptr(J.X, J.Np, k, j), nullptr, nullptr, J.Np);
   __syncthreads();
   doublex4 acc[4];
   gemm64<false>(S0, S1, acc);
-  store_acc_global(tile_ptr(J.W, J.Np, k, j), J.Np, acc, 1.0, false);
+  if (J.xw) store_acc_global<C>(tile_ptr(J.W, J.Np, k, j), J.Np, acc, 1.0, false);
   if (J.fout) {
     __syncthreads();  // S1 fully read by the GEMM
     store_acc_lds(S1, acc);
@@ -488,6 +535,11 @@ __global__ __launch_bounds__(NTHREADS) void inv_step(InvArgs args) {
     int ti, tj;
     tri_decode(local, ti, tj);
     if (local == 0 && threadIdx.x == 0 && J.info) *J.info = 0;
+    if (J.cnt) {  // inv_flow follows: its counters start at 0 (diag[0] set below)
+      if (threadIdx.x == 0) J.cnt[ti * T + tj] = J.cnt[T * T + ti * T + tj] = 0u;
+      if (local == 0 && threadIdx.x < T) J.cnt[2 * T * T + threadIdx.x] = 0u;
+      if (jb == 0 && local == 0 && threadIdx.x < 2 && args.flow) args.flow[threadIdx.x] = 0u;
+    }
     build_tile(J, ti, tj, reinterpret_cast<float*>(S0), reinterpret_cast<float*>(S1),
                local == 0 ? S2 : nullptr);
     if (J.fout && ti != tj) emit_zero_block(J, ti, tj);
@@ -508,6 +560,196 @@ __global__ __launch_bounds__(NTHREADS) void inv_step(InvArgs args) {
   check_pivots(J, d, dg);
   store_tile(tile_ptr(J.X, J.Np, d, d), S1, J.Np);
   if (J.fout) emit_out(J, d, d, S1);
+  if (J.cnt && d == 0 && threadIdx.x == 0) J.cnt[2 * T * T] = 1u;  // X[0][0] ready for inv_flow
+}
+
+// ------------------------------------------- dataflow steps (one persistent launch)
+// inv_flow runs every step k >= 0 of the merged elimination (after the build launch,
+// inv_step(-1)) as ONE launch of a few workgroups that dequeue tasks in step order
+// from a counter and start each as soon as the tiles it reads are final, instead
+// of one launch per step: no kernel boundary per step, and a handful of resident
+// workgroups (not ~100 per step) — the inversion keeps its CUs while the next data
+// pass's SYRK launches fill the rest of the chip.
+// Per job, counters written only by the task that finalises the tile (one writer each):
+//   verR[i*T+j] = k + 1 once R'[i][j] holds the trailing updates of steps 0..k
+//   verZ[i*T+j] = k - j + 1 once Z[i][j] holds the updates of steps j..k
+//   diag[k]     = 1 once X[k][k] is stored
+// Task (k, ...) needs X[k][k] and its operand tiles updated through step k-1:
+//   trailing (i, j): verR[i][k], verR[j][k], verR[i][j] >= k
+//   Z (i, j):        verR[i][k] >= k, verZ[k][j] >= k - j (j < k), verZ[i][j] >= k - j
+//   last row (j):    verZ[T-1][j] >= T - 1 - j
+// Dequeue order (topological, so every awaited task is held by a running
+// workgroup: any number of resident workgroups completes, no co-residency assumed):
+// the diagonal chain runs one step ahead of the bulk.  With D_k = trailing (k+1, k+1)
+// of step k (it factors X[k+1][k+1]) and F_k = trailing (k+2, k+1), (k+2, k+2) of
+// step k (the tiles D_{k+1} reads), segment s holds, per job,
+//   D_s,  the rest of step s-1,  F_s            (segment 0: D_0, F_0)
+// (segment T: the last row), so D_{s+1} is queued right behind the step-s tasks it
+// needs instead of behind all of step s, and the bulk of a step runs while the
+// next diagonal tile is factored.
+// (vmcnt(0) in every wave), meets the workgroup barrier, then one lane stores the
+// counter.  Waits are bounded (1 s): a timeout sets the abort word and info = -1.
+constexpr int FLOW_SEGS = MERGE_T + 1;
+
+// tasks of step k (T tiles per edge); its critical ones (D_k and, if present, F_k);
+// the rest of it (the last row, k = T-1, has no critical task)
+__host__ __device__ inline int flow_step_tasks(int T, int k) {
+  return k + 1 < T ? (T - k - 1) * (T - k) / 2 + (T - k - 1) * (k + 1) : (k + 1 == T ? k : 0);
+}
+__host__ __device__ inline int flow_crit(int T, int k) {
+  return k + 1 < T ? ((T - k - 1) * (T - k) / 2 >= 3 ? 3 : 1) : 0;
+}
+__host__ __device__ inline int flow_rest(int T, int k) { return flow_step_tasks(T, k) - flow_crit(T, k); }
+
+struct FlowArgs {
+  InvArgs a;
+  int total;  // tasks
+  int nsegs;  // Tmax + 1
+  int sbegin[FLOW_SEGS][IMAXJ + 1];  // first task of (segment s, job j); [s][njobs] = end of segment s
+};
+
+__device__ __forceinline__ unsigned cnt_ld(const unsigned* p) {
+  return __hip_atomic_load((gunsigned*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void cnt_st(unsigned* p, unsigned v) {
+  __hip_atomic_store((gunsigned*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One wave (all lanes, one address): spin until *p >= need (false: aborted / timed
+// out).  Every value is read back through readfirstlane, so the loop is uniform.
+__device__ __forceinline__ unsigned cnt_ld_u(const unsigned* p) {
+  return __builtin_amdgcn_readfirstlane(cnt_ld(p));
+}
+__device__ bool flow_wait(const unsigned* p, unsigned need, unsigned* abort_word) {
+  if (cnt_ld_u(p) >= need) return true;
+  const uint64_t deadline = __builtin_amdgcn_s_memrealtime() + 100000000ull;  // 1 s at 100 MHz
+  for (;;) {
+    __builtin_amdgcn_s_sleep(1);
+    if (cnt_ld_u(p) >= need) return true;
+    if (cnt_ld_u(abort_word)) return false;
+    if (__builtin_amdgcn_s_memrealtime() > deadline) {
+      cnt_st(abort_word, 1u);
+      return false;
+    }
+  }
+}
+
+__global__ __launch_bounds__(NTHREADS) void inv_flow(FlowArgs fa) {
+  __shared__ __attribute__((aligned(16))) double S0[NB * DP];
+  __shared__ __attribute__((aligned(16))) double S1[NB * DP];
+  __shared__ __attribute__((aligned(16))) double S2[NB * DP];
+  __shared__ double dg[NB + 352];
+  __shared__ int s_task, s_ok;
+  const InvArgs& args = fa.a;
+  unsigned* head = args.flow;
+  unsigned* abort_word = args.flow + 1;
+  // All control below is wave-uniform (scalar conditions): wave 0 dequeues, waits
+  // and publishes with all its lanes, so no divergent branch encloses a loop exit
+  // or a barrier (a `threadIdx.x == 0` region at the loop head made the compiler
+  // split wave 0's lanes over two loop nests and run its barriers twice: a hang).
+  const bool lead = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
+  for (;;) {
+    if (lead) {
+      // lane 0 adds 1, the others 0: lane 0's old value is this workgroup's task
+      const unsigned old = __hip_atomic_fetch_add((gunsigned*)head, (threadIdx.x == 0) ? 1u : 0u,
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_task = (int)__builtin_amdgcn_readfirstlane(old);
+    }
+    __syncthreads();
+    // uniform (scalar) loop control: with a VGPR task index the compiler treats the
+    // loop exits as divergent and may run one wave's barriers on different trips for
+    // different lanes (a barrier-count mismatch: the workgroup hangs)
+    const int t = __builtin_amdgcn_readfirstlane(s_task);
+    if (t >= fa.total) break;
+    int sg = 0;
+    while (t >= fa.sbegin[sg][args.njobs]) ++sg;
+    int jb = 0;
+    while (jb + 1 < args.njobs && t >= fa.sbegin[sg][jb + 1]) ++jb;
+    const InvJobDev& J = args.job[jb];
+    const int T = J.T;
+    int u = t - fa.sbegin[sg][jb];
+    const unsigned* verR = J.cnt;
+    const unsigned* verZ = J.cnt + T * T;
+    unsigned* cnt = J.cnt;
+    // (step k, step-local index lo) of the task, see the segment layout above
+    int k, lo;
+    const bool hasA = sg <= T - 2;
+    if (hasA && u == 0) {
+      k = sg;
+      lo = 0;
+    } else {
+      u -= hasA ? 1 : 0;
+      const int nB = sg >= 1 ? flow_rest(T, sg - 1) : 0;
+      if (u < nB) {
+        k = sg - 1;
+        lo = u + flow_crit(T, k);
+      } else {
+        k = sg;
+        lo = 1 + (u - nB);
+      }
+    }
+    // task kind: 0 trailing, 1 Z, 2 last row; (i, j) its tile
+    const int nTrail = (T - k - 1) * (T - k) / 2;
+    int kind, i, j;
+    if (k == T - 1) {
+      kind = 2;
+      i = k;
+      j = lo;
+    } else if (lo < nTrail) {
+      int a, b;
+      tri_decode(lo, a, b);
+      kind = 0;
+      i = k + 1 + a;
+      j = k + 1 + b;
+    } else {
+      const int z = lo - nTrail;
+      kind = 1;
+      i = k + 1 + z / (k + 1);
+      j = z % (k + 1);
+    }
+    if (lead) {
+      bool ok = flow_wait(cnt + 2 * T * T + k, 1u, abort_word);
+      if (kind == 0) {
+        ok = ok && flow_wait(verR + i * T + k, k, abort_word);
+        ok = ok && flow_wait(verR + j * T + k, k, abort_word);
+        ok = ok && flow_wait(verR + i * T + j, k, abort_word);
+      } else if (kind == 1) {
+        ok = ok && flow_wait(verR + i * T + k, k, abort_word);
+        if (j < k) ok = ok && flow_wait(verZ + k * T + j, k - j, abort_word);
+        ok = ok && flow_wait(verZ + i * T + j, k - j, abort_word);
+      } else {
+        ok = ok && flow_wait(verZ + i * T + j, T - 1 - j, abort_word);
+      }
+      if (!ok)
+        for (int q = 0; q < args.njobs; ++q)
+          if (args.job[q].info) __hip_atomic_store(args.job[q].info, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_ok = ok;
+    }
+    __syncthreads();
+    if (!__builtin_amdgcn_readfirstlane(s_ok)) break;
+    bool factored = false;
+    if (kind == 0) {
+      if (step_trailing<true>(J, k, lo, S0, S1, S2)) {
+        const int d = k + 1;
+        diag_factor(S2, S1, dg);
+        check_pivots(J, d, dg);
+        store_tile<true>(tile_ptr(J.X, J.Np, d, d), S1, J.Np);
+        emit_out(J, d, d, S1);
+        factored = true;
+      }
+    } else if (kind == 1) {
+      step_z<true>(J, k, lo - nTrail, S0, S1, S2);
+    } else {
+      step_last_row<true>(J, k, j, S0, S1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's tile stores have landed
+    __syncthreads();                                    // ... and every other wave's
+    if (lead) {  // every lane of wave 0 stores the same word
+      if (kind == 0) cnt_st(cnt + i * T + j, (unsigned)(k + 1));
+      else if (kind == 1) cnt_st(cnt + T * T + i * T + j, (unsigned)(k - j + 1));
+      if (factored) cnt_st(cnt + 2 * T * T + k + 1, 1u);
+    }
+  }
 }
 
 // ------------------------------------------- two-launch step (large factors)
@@ -667,9 +909,24 @@ __global__ __launch_bounds__(NTHREADS) void inv_out(InvArgs args) {
 }
 
 // ---------------------------------------------------------------- host side
+// inv_flow counters of a job (verR, verZ, diag) + the group's queue header
+static size_t flow_cnt_bytes(int64_t T) { return align_up((size_t)(2 * T * T + T + 2) * sizeof(unsigned), 256); }
+
 static size_t job_ws(const kfac_invert_job& j) {
-  const int64_t Np = cdiv(j.n, NB) * NB;
-  return 3 * align_up((size_t)(Np * Np) * sizeof(double), 256);
+  const int64_t T = cdiv(j.n, NB), Np = T * NB;
+  return 3 * align_up((size_t)(Np * Np) * sizeof(double), 256) + flow_cnt_bytes(T);
+}
+
+// inv_flow (KFAC_INV_FLOW=1) or one launch per step (default: on the MLP the
+// per-step launches are as fast at >= 64 flow workgroups and faster below, since a
+// merged-step task recomputes its panels: ~12 us per task); workgroups of the
+// persistent launch: KFAC_INV_FLOW_WGS (default 64)
+static int flow_wgs() {
+  const char* e = getenv("KFAC_INV_FLOW");
+  if (!e || e[0] != '1') return 0;
+  const char* w = getenv("KFAC_INV_FLOW_WGS");
+  const int n = w ? atoi(w) : 64;
+  return n > 0 ? n : 64;
 }
 
 template <typename Count>
@@ -712,7 +969,8 @@ static int invert_group(const kfac_invert_job* jobs, int njobs, char* ws, int32_
     d.W = reinterpret_cast<double*>(ws);
     d.X = reinterpret_cast<double*>(ws + mat);
     d.Tm = reinterpret_cast<double*>(ws + 2 * mat);
-    ws += 3 * mat;
+    d.cnt = reinterpret_cast<unsigned*>(ws + 3 * mat);
+    ws += 3 * mat + flow_cnt_bytes(d.T);
     Tmax = std::max(Tmax, d.T);
     any_inverse |= jb.out_kind == KFAC_OUT_INVERSE;
   }
@@ -725,6 +983,36 @@ static int invert_group(const kfac_invert_job* jobs, int njobs, char* ws, int32_
     all_fused &= args.job[i].fout != 0;
   }
   int rc;
+  const bool flow = all_fused && flow_wgs() > 0;
+  if (flow) {  // build launch, then every step in one persistent dataflow launch
+    // final X[k][j] tiles are never stored (the steps emit L directly): W[k][j] may
+    // still be read as R'[k][j] by a step-j task still running
+    for (int i = 0; i < njobs; ++i) args.job[i].xw = 0;
+    args.flow = args.job[0].cnt + 2 * args.job[0].T * args.job[0].T + args.job[0].T;
+    if (!phase) {
+      args.step = -1;
+      return launch(inv_step, args, [](const InvJobDev& d) { return d.T * (d.T + 1) / 2; }, s);
+    }
+    FlowArgs fa{};
+    fa.a = args;
+    fa.nsegs = Tmax + 1;
+    int total = 0;
+    for (int sg = 0; sg <= Tmax; ++sg) {
+      for (int i = 0; i < njobs; ++i) {
+        const int T = args.job[i].T;
+        fa.sbegin[sg][i] = total;
+        if (sg <= T - 2) total += flow_crit(T, sg);   // D_s (+ F_s)
+        if (sg >= 1) total += flow_rest(T, sg - 1);   // the rest of step s-1
+      }
+      fa.sbegin[sg][njobs] = total;
+    }
+    fa.total = total;
+    if (total == 0) return KFAC_OK;
+    hipLaunchKernelGGL(inv_flow, dim3(std::min(total, flow_wgs())), dim3(NTHREADS), 0, s, fa);
+    KFAC_CHECK_LAUNCH();
+    return KFAC_OK;
+  }
+  for (int i = 0; i < njobs; ++i) args.job[i].cnt = nullptr;
   // info is zeroed by the first launch (workgroup 0 of each job)
   if (merged) {
     for (int k = phase ? 0 : -1; k < (phase ? Tmax : 0); ++k) {

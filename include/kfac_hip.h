@@ -224,6 +224,10 @@ KFAC_API int kfac_profile_reset(void);
  * inversion of the previous pass on disjoint CU sets, so neither waits for the
  * other's workgroups to drain from a CU.  kfac_cu_count: the device's CUs.   */
 KFAC_API int kfac_cu_count(int device, int* count);
+/* CUs the factor (SYRK) launches are planned for: 4 resident workgroups per CU,
+ * split-K sized to fill them in as few rounds as possible.  0 = the whole chip
+ * (256).  Lower it when the launches run on a CU-masked stream.              */
+KFAC_API int kfac_set_cu_budget(int cus);
 KFAC_API int kfac_stream_create_cu_mask(const uint32_t* mask, int words, void** stream);
 KFAC_API int kfac_stream_destroy(void* stream);
 

@@ -164,6 +164,7 @@ def test_overlapped_inversion_matches_serial(hip_device):
     def run(overlap):
         kfac = KFAC(net)
         kfac.overlap_invert = overlap
+        kfac.partition_cus = 0  # one stream layout: same SYRK splits as the serial path
         kept = []
         for batches in passes:
             kfac.reset()
@@ -188,3 +189,79 @@ def test_overlapped_inversion_matches_serial(hip_device):
     R = O.damped_factor(ref.state["l0"][0], 0.04, 200)
     L = serial[0][0].astype(np.float64)
     assert np.abs(L.T @ R @ L - np.eye(R.shape[0])).max() < 1e-3
+
+
+@pytest.mark.parametrize("wgs", ["1", "7", "32", "200"])
+def test_flow_inversion_equals_per_step_launches(hip_device, monkeypatch, wgs):
+    """inv_flow (one persistent dataflow launch for every elimination step, any number
+    of workgroups — one included) gives the per-step launches' factors bit for bit."""
+    from bnn_kfac_amd import _native as N
+    rng = np.random.default_rng(11)
+    sizes = (785, 128, 129, 10, 1536, 64, 65)
+    mats = [_t(_spd(n, rng, 1e4), hip_device) for n in sizes]
+
+    def run(flow):
+        monkeypatch.setenv("KFAC_INV_FLOW", flow)
+        monkeypatch.setenv("KFAC_INV_FLOW_WGS", wgs)
+        outs = [torch.empty_like(F) for F in mats]
+        info = N.invert([N.invert_job(F, o, 200 ** 0.5, 0.04 ** 0.5) for F, o in zip(mats, outs)],
+                        hip_device)
+        torch.cuda.synchronize()
+        assert not info.cpu().any()
+        return outs
+
+    ref, got = run("0"), run("1")
+    for n, a, b in zip(sizes, ref, got):
+        assert torch.equal(a, b), n
+    F = mats[0].cpu().numpy()
+    np.testing.assert_allclose(got[0].cpu().numpy(), O.invert_factor(F, 0.04, 200), rtol=1e-4,
+                               atol=1e-7 * float(got[0].abs().max()))
+
+
+def test_cu_partitioned_passes_match_serial(hip_device):
+    """overlap_invert with the CU partition (opt-in): a pass that starts while the
+    previous inversion runs is launched on the data CUs' stream with its SYRK planned
+    for them (other K-splits: fp32 sums within rounding of the serial path's), the
+    inversion on its own CUs; every pass's L satisfies L^T R L = I on its own factors."""
+    from bnn_kfac_amd.curvatures import KFAC
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Linear(784, 128), nn.ReLU(), nn.Linear(128, 10)).to(hip_device)
+    g = torch.Generator(device=hip_device).manual_seed(5)
+    passes = [[(torch.rand(4096, 784, device=hip_device, generator=g),
+                torch.randn(4096, 128, device=hip_device, generator=g),
+                torch.rand(4096, 128, device=hip_device, generator=g),
+                torch.randn(4096, 10, device=hip_device, generator=g)) for _ in range(4)]
+              for _ in range(4)]
+
+    def run(overlap):
+        kfac = KFAC(net)
+        kfac.overlap_invert = overlap
+        kfac.partition_cus = 32
+        states, invs, used = [], [], []
+        for batches in passes:
+            kfac.reset()
+            for a1, g1, a2, g2 in batches:
+                kfac.record[net[0]] = [a1, g1]
+                kfac.record[net[2]] = [a2, g2]
+                kfac.update(a1.shape[0])
+                used.append(kfac._cycle_stream is not None)
+            kfac.invert(0.04, 200)
+            states.append([t.clone() for pair in kfac.state.values() for t in pair])
+            invs.append(dict(kfac._inv_state))
+        _ = kfac.inv_state
+        torch.cuda.synchronize()
+        return ([[t.cpu().numpy() for t in st] for st in states],
+                [[t.cpu().numpy() for pair in d.values() for t in pair] for d in invs], any(used))
+
+    s_state, s_inv, _ = run(False)
+    with torch.cuda.stream(torch.cuda.Stream(hip_device)):  # the partition needs a non-default stream
+        p_state, p_inv, used = run(True)
+    assert used, "no pass ran on the partition's data stream"
+    for want_pass, got_pass in zip(s_state, p_state):
+        for want, got in zip(want_pass, got_pass):
+            np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-6 * np.abs(want).max())
+    for st, inv in zip(p_state, p_inv):
+        for F, L in zip(st, inv):
+            R = O.damped_factor(F.astype(np.float64), 0.04, 200)
+            Ld = L.astype(np.float64)
+            assert np.abs(Ld.T @ R @ Ld - np.eye(R.shape[0])).max() < 1e-3
