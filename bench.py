@@ -149,7 +149,7 @@ def main():
     ap.add_argument("--images", type=int, default=60000, help="images per rank per pass")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--partition", type=int, default=32,
+    ap.add_argument("--partition", type=int, default=0,
                     help="CUs reserved for the overlapped inversion (KFAC.partition_cus; 0 = none)")
     args = ap.parse_args()
 

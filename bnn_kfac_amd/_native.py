@@ -7,6 +7,7 @@ on the tensor's device, passed to every call explicitly.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import threading
@@ -249,7 +250,26 @@ def cu_mask_stream(device: torch.device, cus) -> "torch.cuda.ExternalStream":
     with torch.cuda.device(device):
         check(lib().kfac_stream_create_cu_mask(mask, words, ctypes.byref(handle)),
               "kfac_stream_create_cu_mask")
+    if not _mask_streams:
+        atexit.register(_destroy_mask_streams)
+    _mask_streams.append((device, handle.value))
     return torch.cuda.ExternalStream(handle.value, device=device)
+
+
+_mask_streams = []
+
+
+def _destroy_mask_streams():
+    """Drain and destroy the CU-masked streams before the HIP runtime tears down
+    (left to the runtime's own teardown, it crashed under rocprofv3)."""
+    while _mask_streams:
+        device, handle = _mask_streams.pop()
+        try:
+            torch.cuda.synchronize(device)
+            lib().kfac_stream_destroy(c_vp(handle))
+        except Exception:  # interpreter shutdown: best effort
+            pass
+
 
 
 def syev(jobs, device: torch.device) -> torch.Tensor:

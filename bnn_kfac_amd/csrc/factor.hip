@@ -43,6 +43,7 @@ struct FactorArgs {
   const float* segs[KSEG];  // batch bases of the multi-batch jobs (kernel arguments: no copy)
   int njobs;
   int stagger;  // start delay per dispatch round, in 512-cycle s_sleep(8) units
+  int split_major;  // LDS-DMA path task order: 1 split-major, 0 tile-major (KFAC_SYRK_ORDER)
   int task_end[MAXJ];
   int tile_end[MAXJ];
   FactorJobDev job[MAXJ];
@@ -241,9 +242,15 @@ __device__ __forceinline__ void stage_barrier() {
 // MFMAs off the 64-cycle dependent-accumulator latency.
 template <int GBK, int NSLOT, int NACC, int MODE = 0, int SUB = 1>
 __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, const float* const* segs,
-                                                 int local, float* lds) {
+                                                 int local, float* lds, int split_major) {
   static_assert(NSLOT >= 2 * SUB, "ring must hold the computed step and the next one");
-  const int tile = local / J.splits, split = local - tile * J.splits;
+  // split-major order: xcd_task hands every XCD a contiguous range of K-splits of
+  // ALL tiles, so each XCD streams ~1/8 of the operand rows through its L2 once
+  // (tile-major gave every XCD all K of its tiles' panels: ~8x the HBM fetch on
+  // the multi-batch launches of a queued pass)
+  const int ntiles = J.t * (J.t + 1) / 2;
+  const int split = split_major ? local / ntiles : local % J.splits;
+  const int tile = split_major ? local - split * ntiles : local / J.splits;
   int ti, tj;
   tri_decode(tile, ti, tj);
   const int64_t s0 = (int64_t)split * J.chunk;
@@ -396,7 +403,7 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
   if constexpr (FAMILY == KFAC_ROWMAJOR) {
     const float* const* segs = args.segs;
     if (J.glds)
-      factor_task_glds<GBK, NSLOT, 1, MODE, SUB>(J, segs, local, lds);
+      factor_task_glds<GBK, NSLOT, 1, MODE, SUB>(J, segs, local, lds, args.split_major);
     else
       factor_task<KFAC_ROWMAJOR>(J, segs, local, lds);
   } else {
@@ -903,6 +910,10 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
   FactorArgs red{};  // the reduce launch: jobs reduced now (no accumulator)
   args.njobs = njobs;
   args.stagger = 5;
+  {
+    const char* e = getenv("KFAC_SYRK_ORDER");
+    args.split_major = e ? atoi(e) : 1;
+  }
   int tasks = 0, rtiles = 0, nsegs = 0;
   size_t off = 0;
   for (int i = 0; i < njobs; ++i) {

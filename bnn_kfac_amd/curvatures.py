@@ -202,12 +202,14 @@ class KFAC(Curvature):
         self.partition_cus = 0
         self._part = {}           # device index -> (data stream, inversion stream, data CUs) | False
         self._cycle_stream = None  # data stream of the pending cycle (None: the caller's stream)
+        self._cycle_hold = []      # (event on it, records its launches read) until they ran
 
     def reset(self):
         """Forget the accumulated factors (start a new data pass); device buffers are kept."""
         if getattr(self, "_cycle_stream", None) is not None:  # a dropped cycle: keep later work behind it
             torch.cuda.current_stream(self._acc_device).wait_stream(self._cycle_stream)
             self._cycle_stream = None
+            self._cycle_hold = []
         self._queue = []
         self._launch_at = 1
         self._fast = None
@@ -234,6 +236,7 @@ class KFAC(Curvature):
         ds, self._cycle_stream = self._cycle_stream, None
         if ds is not None:
             torch.cuda.current_stream(device).wait_stream(ds)
+        self._cycle_hold = []
 
     def _partition(self, device):
         """(data stream, inversion stream, data CUs) of the CU partition, or None."""
@@ -258,26 +261,40 @@ class KFAC(Curvature):
         caller's stream and the whole chip."""
         part = self._partition(device)
         pend = self._inv_pending
-        busy = (part is not None and pend is not None and pend[5] and not pend[0].query())
+        busy = (part is not None and pend is not None and pend[6] and not pend[0].query())
         self._cycle_stream = part[0] if busy else None
         if part is not None:
             N.set_cu_budget(part[2] if busy else 0)
-        if busy:
-            for t in (self._packed, self._acc_buf):
-                if t is not None:
-                    t.record_stream(part[0])
 
     def _on_cycle_stream(self, device, fn, keep=()):
-        """Run the launch(es) of `fn` on the cycle's stream, behind the caller's work;
-        the records it reads stay allocated until that stream has run them."""
+        """Run the launch(es) of `fn` on the cycle's stream, behind the caller's work.
+        The records it reads are held until an event behind the launch has completed
+        (or the caller's stream has waited for the cycle): their memory, owned by the
+        caller's stream, is not reused under the launch.  (No record_stream: the
+        allocator's events on a CU-masked stream crashed interpreter teardown under
+        rocprofv3.)  The buffers the launches write (`_packed`, the accumulators) are
+        replaced only at a cycle start, after the caller's stream waited for the last."""
         ds = self._cycle_stream
+        pend = self._inv_pending
+        if ds is not None and (pend is None or pend[0].query()):
+            # the inversion has finished: the rest of the cycle runs on the caller's
+            # stream over the whole chip (a long pass keeps only its first launches
+            # on the data CUs; the K-splits stay as planned)
+            cur = torch.cuda.current_stream(device)
+            cur.wait_stream(ds)
+            self._cycle_stream, self._cycle_hold, ds = None, [], None
         if ds is None:
             return fn()
         ds.wait_stream(torch.cuda.current_stream(device))
         with torch.cuda.stream(ds):
             fn()
-        for t in keep:
-            t.record_stream(ds)
+        hold = self._cycle_hold
+        while hold and hold[0][0].query():
+            hold.pop(0)
+        if keep:
+            ev = torch.cuda.Event()
+            ev.record(ds)
+            hold.append((ev, list(keep)))
 
     # curvatures.py:319-323
     def _save_input(self, module, input):
@@ -527,8 +544,6 @@ class KFAC(Curvature):
             buf = self._acc_buf
             if buf is None or buf.device != device or buf.numel() < total:
                 buf = self._acc_buf = torch.empty(total, dtype=torch.uint8, device=device)
-                if self._cycle_stream is not None:
-                    buf.record_stream(self._cycle_stream)
             base = buf.data_ptr()
             self._acc_map, self._acc_live, flush = {}, set(), []
             for j, (splits, _nbytes), off in zip(uniq, plan, offs):
@@ -575,7 +590,12 @@ class KFAC(Curvature):
         # stream waits only until the factors have been READ (kfac_invert_ex's
         # inputs_read event, after the first launch), so it may overwrite them.
         main = torch.cuda.current_stream(device)
-        side = self._side_stream(device) if self.overlap_invert else main
+        # the CU partition only for latency-bound inversions (every factor within the
+        # one-launch-per-step range, <= 24 tiles of 64): a large factor's inversion is
+        # throughput-bound and needs the whole chip (wide MLP, 4097^2: 4x slower on 32 CUs)
+        part = self._partition(device) if self.overlap_invert else None
+        part_side = part is not None and max(F_.shape[0] for _, v in entries for F_ in v) <= 24 * 64
+        side = (part[1] if part_side else self._side_stream(device)) if self.overlap_invert else main
         read = None
         if side is not main:
             side.wait_stream(main)
@@ -598,22 +618,36 @@ class KFAC(Curvature):
             host = self._info_host
             if host is None or host.numel() != info.numel():
                 host = self._info_host = torch.empty(info.numel(), dtype=info.dtype, pin_memory=True)
-            host.copy_(info, non_blocking=True)
             done = torch.cuda.Event()
             done.record(side)
+            # the copy goes on an ordinary torch stream: the pinned-memory allocator's
+            # stream bookkeeping must not name a CU-masked (library-owned) stream
+            cs = self._copy_stream(device) if part_side else side
+            if cs is not side:
+                cs.wait_event(done)
+            with torch.cuda.stream(cs):
+                host.copy_(info, non_blocking=True)
+            if cs is not side:
+                done = torch.cuda.Event()
+                done.record(cs)
         if read is not None:
             main.wait_event(read)
         for layer, pair in outs:
             self._inv_state[layer] = pair
         self._inv_pending = (done, host, [layer for layer, _ in outs], self._inv_state,
-                             [t for _, pair in outs for t in pair], side is not main)
+                             [t for _, pair in outs for t in pair], side is not main, part_side)
+
+    def _copy_stream(self, device):
+        s = getattr(self, "_copy_streams", {}).get(device.index)
+        if s is None:
+            self._copy_streams = getattr(self, "_copy_streams", {})
+            s = self._copy_streams[device.index] = torch.cuda.Stream(device=device)
+        return s
 
     def _side_stream(self, device):
         s = self._inv_streams.get(device.index)
         if s is None:
-            part = self._partition(device)
-            s = part[1] if part is not None else torch.cuda.Stream(device=device, priority=-1)
-            self._inv_streams[device.index] = s
+            s = self._inv_streams[device.index] = torch.cuda.Stream(device=device, priority=-1)
         return s
 
     def _check_inverse(self):
@@ -625,7 +659,7 @@ class KFAC(Curvature):
         if pending is None:
             return
         self._inv_pending = None
-        done, host, layers, target, outs, on_side = pending
+        done, host, layers, target, outs, on_side, _ = pending
         done.synchronize()
         if on_side:
             # later work on the reading stream sees the finished factors, and the

@@ -25,7 +25,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    return name.split("(")[0].replace("kfac::", "")
+    """'void kfac::kfac_factor_tiles_t<32, 2, 2, 1>(kfac::FactorArgs)' -> 'kfac_factor_tiles'"""
+    base = name.split("(")[0].split("<")[0].replace("void ", "").replace("kfac::", "").strip()
+    return base[:-2] if base.endswith("_t") else base
 
 
 def main(tag):
@@ -40,6 +42,10 @@ def main(tag):
             vals[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
         for (k, c), v in vals.items():
             pmc[k][c] = {"mean_per_dispatch": sum(v) / len(v), "dispatches": len(v)}
+    # the kernel-trace stats of the same bench command (mean launch time per kernel)
+    stats = {}
+    for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
+        stats[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3}
     with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
         json.dump(pmc, f, indent=1, sort_keys=True)
     t = pmc.get("kfac_factor_tiles", {})
@@ -48,6 +54,7 @@ def main(tag):
         write = t["WRITE_SIZE"]["mean_per_dispatch"] * 1024
         out = {"kernel": "kfac_factor_tiles", "tag": tag, "fetch_bytes_per_launch": fetch,
                "write_bytes_per_launch": write, "hbm_bytes_per_launch": fetch + write,
+               "rocprof_trace": stats.get("kfac_factor_tiles"),
                "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->bytes, "
                        "mean over the bench's launches (15 updates per pass, last batch short)"}
         with open(os.path.join(ROOT, "profiles", "factor_tiles_pmc.json"), "w") as f:
