@@ -389,7 +389,11 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, const fl
 template <int GBK, int NSLOT, int MODE = 0, int SUB = 1, int FAMILY = KFAC_ROWMAJOR>
 __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs args) {
   constexpr int RING = FAMILY == KFAC_ROWMAJOR ? NSLOT * 2 * GBK * TILE : 0;
-  __shared__ __attribute__((aligned(16))) float lds[(4 * PANEL > RING) ? 4 * PANEL : RING];
+  // MODE & 256: every job takes the LDS-DMA path, the ring is all the LDS (32 KB, not
+  // the register-staged path's 34 KB): 4 resident workgroups leave 32 KB of a CU's
+  // 160, room for a 32-tile inversion workgroup (29 KB) of an overlapped invert()
+  constexpr int LDSF = (MODE & 256) ? RING : ((4 * PANEL > RING) ? 4 * PANEL : RING);
+  __shared__ __attribute__((aligned(16))) float lds[LDSF];
   // Workgroups of later dispatch rounds (blockIdx / 256: the ~4 sharing a CU) start a
   // fraction of a stage later, so their DMA waits and barriers interleave instead of
   // stalling all 16 waves of a CU together (measured +2.5% on the MLP update).
@@ -402,7 +406,9 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
   const int local = task - J.task_begin;
   if constexpr (FAMILY == KFAC_ROWMAJOR) {
     const float* const* segs = args.segs;
-    if (J.glds)
+    if constexpr ((MODE & 256) != 0)
+      factor_task_glds<GBK, NSLOT, 1, MODE, SUB>(J, segs, local, lds, args.split_major);
+    else if (J.glds)
       factor_task_glds<GBK, NSLOT, 1, MODE, SUB>(J, segs, local, lds, args.split_major);
     else
       factor_task<KFAC_ROWMAJOR>(J, segs, local, lds);
@@ -414,6 +420,7 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
 // production configuration: 32-row stages, 2-slot ring (one stage in flight),
 // DS reads interleaved with the MFMAs (MODE 2: -1.2 us of 42 on the MLP update)
 #define kfac_factor_tiles kfac_factor_tiles_t<32, 2, 2>
+#define kfac_factor_tiles_glds kfac_factor_tiles_t<32, 2, 2 | 256>
 #define kfac_factor_tiles_channel kfac_factor_tiles_t<32, 2, 2, 1, KFAC_CHANNEL>
 #define kfac_factor_tiles_patch kfac_factor_tiles_t<32, 2, 2, 1, KFAC_PATCH>
 
@@ -967,7 +974,14 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
           hipLaunchKernelGGL(kfac_factor_tiles_patch, dim3(tasks), dim3(NTHREADS), 0, stream, args);
         break;
       default:
-        hipLaunchKernelGGL(kfac_factor_tiles, dim3(tasks), dim3(NTHREADS), 0, stream, args);
+        {
+          bool all_glds = true;
+          for (int i = 0; i < njobs; ++i) all_glds &= args.job[i].glds != 0;
+          if (all_glds)
+            hipLaunchKernelGGL(kfac_factor_tiles_glds, dim3(tasks), dim3(NTHREADS), 0, stream, args);
+          else
+            hipLaunchKernelGGL(kfac_factor_tiles, dim3(tasks), dim3(NTHREADS), 0, stream, args);
+        }
     }
     KFAC_CHECK_LAUNCH();
   }

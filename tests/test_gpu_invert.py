@@ -25,7 +25,7 @@ def _spd(n, rng, cond=1e4):
     return ((q * ev) @ q.T).astype(np.float32)
 
 
-@pytest.mark.parametrize("n", [1, 5, 63, 64, 65, 128, 129, 200, 785])
+@pytest.mark.parametrize("n", [1, 5, 31, 32, 33, 63, 64, 65, 128, 129, 200, 785, 1536, 1537, 2000])
 def test_inv_chol_sizes_vs_fp64(hip_device, n):
     from bnn_kfac_amd import _native as N
     rng = np.random.default_rng(n)

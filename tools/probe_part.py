@@ -74,11 +74,11 @@ def main():
     measure("serial", False, 0)
     measure("overlap, no partition", True, 0)
     measure("overlap, partition 32", True, 32)
-    # the same with every call issued on the data stream itself (as tools/probe_flow.py)
-    kf = KFAC(net)
-    part = kf._partition(dev)
-    with torch.cuda.stream(part[0]):
-        measure("partition 32, caller on data", True, 32)
+    os.environ["KFAC_INV_TILE"] = "64"
+    measure("64-tiles serial", False, 0)
+    measure("64-tiles overlap", True, 0)
+    os.environ.pop("KFAC_INV_TILE")
+    measure("32-tiles overlap again", True, 0)
 
 
 if __name__ == "__main__":
