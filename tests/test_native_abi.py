@@ -62,7 +62,8 @@ def test_workspace_queries_need_no_gpu():
     assert ws >= 91 * 64 * 64 * 4  # at least one slab per lower tile
     inv = N.InvertJob()
     inv.F, inv.ldF, inv.n, inv.out, inv.ldo = 1, 785, 785, 1, 785
-    assert lib.kfac_invert_workspace_bytes(N.as_array(N.InvertJob, [inv]), 1) >= 3 * 832 * 832 * 8
+    # three padded fp64 matrices (32-tiles for n <= 1536: 785 -> 800)
+    assert lib.kfac_invert_workspace_bytes(N.as_array(N.InvertJob, [inv]), 1) >= 3 * 800 * 800 * 8
     # argument validation happens before any launch
     bad = N.FactorJob()
     assert lib.kfac_factor_update(N.as_array(N.FactorJob, [bad]), 1, None, 0, None) == N.KFAC_EINVAL
