@@ -237,6 +237,52 @@ __device__ __forceinline__ void stage_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
+// Narrow row-major factors (n <= 32) whose rows are not 16-B aligned (the MLP's
+// 10-wide output gradient): operands go from global memory straight into the MFMA
+// registers, one stage ahead, so the glds-only launch (32 KB of LDS) takes them
+// too.  Wave w takes rows 8w..8w+7 of every 32-row stage (the 4 waves split K; the
+// store sums them), lane (rr, h) row 2*s2 + h, column rr (the ones column: 1).
+__device__ __forceinline__ void narrow_direct_load(const FactorJobDev& J, const float* base, int64_t k0,
+                                                   float (&v)[BK / 8]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, rr = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int s2 = 0; s2 < BK / 8; ++s2) {
+    const int64_t k = k0 + 2 * (wave * (BK / 8) + s2) + h;
+    v[s2] = k < J.x.rows ? (rr < J.x.cols ? base[k * J.x.ld + rr] : (rr == J.x.ones ? 1.f : 0.f)) : 0.f;
+  }
+}
+
+__device__ __forceinline__ void factor_task_narrow_direct(const FactorJobDev& J, const float* const* segs,
+                                                          int local, float* lds) {
+  const int split = local;  // one tile
+  const int64_t s0 = (int64_t)split * J.chunk;
+  const int64_t s1 = min(J.nst, s0 + J.chunk);
+  floatx16 acc;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+  if (s1 > s0) {
+    StageCursor c;
+    c.init(J, s0);
+    const float* base = seg_base(J, segs, c.seg);
+    float cur[BK / 8], nxt[BK / 8];
+    narrow_direct_load(J, base, c.k, cur);
+    for (int64_t s = s0; s < s1; ++s) {
+      const int seg = c.seg;
+      c.next(J.x.rows);
+      if (s + 1 < s1) {
+        if (c.seg != seg) base = seg_base(J, segs, c.seg);
+        narrow_direct_load(J, base, c.k, nxt);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < BK / 8; ++s2)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[s2], cur[s2], acc, 0, 0, 0);
+#pragma unroll
+      for (int s2 = 0; s2 < BK / 8; ++s2) cur[s2] = nxt[s2];
+    }
+  }
+  store_narrow(J, J.slab + (size_t)split * TILE * TILE, acc, lds);
+}
+
 // NSLOT ring slots (2: one stage in flight, 4 WGs/CU; 3: two in flight, 3 WGs/CU);
 // NACC independent accumulators per wave (k-steps interleaved) to keep back-to-back
 // MFMAs off the 64-cycle dependent-accumulator latency.
@@ -356,6 +402,8 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, const fl
             for (int s2 = 0; s2 < GBK / 2; ++s2)
               acc[s2 % NACC] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s2], bv[s2], acc[s2 % NACC], 0, 0, 0);
           }
+          // (a deeper DS-read lookahead, the reads of MFMA pair t+2..4 issued with pair t,
+          // measured equal: 0.60 ms of tiles per MLP pass either way)
           if (MODE & 2) {
 #pragma unroll
             for (int s2 = 0; s2 < GBK / 2; ++s2) {
@@ -406,8 +454,12 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
   const int local = task - J.task_begin;
   if constexpr (FAMILY == KFAC_ROWMAJOR) {
     const float* const* segs = args.segs;
-    if constexpr ((MODE & 256) != 0)
-      factor_task_glds<GBK, NSLOT, 1, MODE, SUB>(J, segs, local, lds, args.split_major);
+    if constexpr ((MODE & 256) != 0) {
+      if (J.glds)
+        factor_task_glds<GBK, NSLOT, 1, MODE, SUB>(J, segs, local, lds, args.split_major);
+      else
+        factor_task_narrow_direct(J, segs, local, lds);
+    }
     else if (J.glds)
       factor_task_glds<GBK, NSLOT, 1, MODE, SUB>(J, segs, local, lds, args.split_major);
     else
@@ -976,7 +1028,7 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
       default:
         {
           bool all_glds = true;
-          for (int i = 0; i < njobs; ++i) all_glds &= args.job[i].glds != 0;
+          for (int i = 0; i < njobs; ++i) all_glds &= args.job[i].glds != 0 || args.job[i].n <= 32;
           if (all_glds)
             hipLaunchKernelGGL(kfac_factor_tiles_glds, dim3(tasks), dim3(NTHREADS), 0, stream, args);
           else
