@@ -185,7 +185,8 @@ class KFAC(Curvature):
         self._acc_live = set()   # F pointers already written in the pending cycle
         self._acc_flush = None   # flush jobs of the pending cycle (None: nothing pending)
         self._acc_device = None
-        self._info_host = None   # pinned int32 readback of the last inversion's pivot check
+        self._info_pool = []     # free pinned int32 readback buffers of the pivot checks
+        self._inv_older = []     # earlier inversions whose verdict is not read yet (in order)
         self._inv_pending = None  # (event, host info, layers, inv_state dict, outputs, on side
                                   # stream) until settled
         self.overlap_invert = True  # invert() on a side stream (see invert)
@@ -575,7 +576,10 @@ class KFAC(Curvature):
     def invert(self, add: Union[float, list, tuple] = 0., multiply: Union[float, list, tuple] = 1.):
         """L = cholesky(inverse(sqrt(s) F + sqrt(n) I)) per factor (curvatures.py:367-398)."""
         assert self.state, "State dict is empty. Did you call 'update' prior to this?"
-        if self.inv_state:  # (settles the previous inversion's verdict first)
+        # the previous inversion's verdict is read later (no host wait here): its
+        # outputs are ordered before later work on the caller's stream now
+        self._defer_verdict()
+        if self._inv_state:
             Warning("State has already been inverted. Is this expected?")
         damping = self._damping(add, multiply)
         entries = list(self.state.items())
@@ -615,9 +619,10 @@ class KFAC(Curvature):
             # memory; it is settled (event wait) at the next read of `inv_state` or the
             # next invert(), so a data pass can be queued behind this inversion without
             # a host sync in between.
-            host = self._info_host
-            if host is None or host.numel() != info.numel():
-                host = self._info_host = torch.empty(info.numel(), dtype=info.dtype, pin_memory=True)
+            pool = self._info_pool
+            while pool and pool[-1].numel() != info.numel():
+                pool.pop()
+            host = pool.pop() if pool else torch.empty(info.numel(), dtype=info.dtype, pin_memory=True)
             done = torch.cuda.Event()
             done.record(side)
             # the copy goes on an ordinary torch stream: the pinned-memory allocator's
@@ -650,25 +655,49 @@ class KFAC(Curvature):
             s = self._inv_streams[device.index] = torch.cuda.Stream(device=device, priority=-1)
         return s
 
-    def _check_inverse(self):
-        """Settle a pending inversion: a factor that is not positive definite ends as
-        the reference's does (curvatures.py:393-396: torch fails, the numpy fallback
-        raises LinAlgError), the layers from the first failing one on dropped from
-        `inv_state` as the reference never assigns them."""
-        pending = getattr(self, "_inv_pending", None)
-        if pending is None:
-            return
-        self._inv_pending = None
-        done, host, layers, target, outs, on_side, _ = pending
-        done.synchronize()
+    @staticmethod
+    def _order_after(pending):
+        """Later work on the caller's stream sees the inversion's factors, and the
+        allocator keeps their memory until that work has run (no host wait)."""
+        done, _host, _layers, _target, outs, on_side, _ = pending
         if on_side:
-            # later work on the reading stream sees the finished factors, and the
-            # allocator keeps their memory until that work has run
             cur = torch.cuda.current_stream(outs[0].device)
             cur.wait_event(done)
             for t in outs:
                 t.record_stream(cur)
-        bad = host.numpy()
+
+    def _defer_verdict(self):
+        """invert(): queue the pending inversion's verdict instead of waiting for it;
+        read the verdicts that are already back (at most 2 stay queued)."""
+        pending = getattr(self, "_inv_pending", None)
+        if pending is not None:
+            self._inv_pending = None
+            self._order_after(pending)
+            self._inv_older.append(pending)
+        while self._inv_older and (len(self._inv_older) > 2 or self._inv_older[0][0].query()):
+            self._verdict(self._inv_older.pop(0))
+
+    def _check_inverse(self):
+        """Settle every pending inversion, oldest first: a factor that is not positive
+        definite ends as the reference's does (curvatures.py:393-396: torch fails, the
+        numpy fallback raises LinAlgError), the layers from the first failing one on
+        dropped from `inv_state` as the reference never assigns them."""
+        older = getattr(self, "_inv_older", [])
+        while older:
+            self._verdict(older.pop(0))
+        pending = getattr(self, "_inv_pending", None)
+        if pending is None:
+            return
+        self._inv_pending = None
+        self._order_after(pending)
+        self._verdict(pending)
+
+    def _verdict(self, pending):
+        """Wait for one inversion's pivot check and act on it."""
+        done, host, layers, target, outs, on_side, _ = pending
+        done.synchronize()
+        bad = host.numpy().copy()
+        self._info_pool.append(host)
         if (bad < 0).any():
             target.clear()
             raise RuntimeError("kfac_invert: the inversion work queue timed out (no result)")
