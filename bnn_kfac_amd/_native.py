@@ -85,6 +85,8 @@ SIGNATURES = {
                                                         c_i64]),
     "kfac_kron_quadform": (ctypes.c_int, [ctypes.POINTER(QuadJob), ctypes.c_int, c_i64,
                                           ctypes.c_int, c_vp, c_vp, ctypes.c_size_t, c_vp]),
+    "kfac_invert_phase": (ctypes.c_int, [ctypes.POINTER(InvertJob), ctypes.c_int, c_vp, ctypes.c_size_t,
+                                         c_vp, ctypes.c_int, c_vp]),
     "kfac_cu_count": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "kfac_set_cu_budget": (ctypes.c_int, [ctypes.c_int]),
     "kfac_stream_create_cu_mask": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
@@ -225,6 +227,21 @@ def invert(jobs, device: torch.device, inputs_read=None) -> torch.Tensor:
     check(L.kfac_invert_ex(arr, len(jobs), ws.data_ptr(), ws.numel(), info.data_ptr(), ev, stream),
           "kfac_invert_ex")
     return info
+
+
+def invert_prepare(jobs, device: torch.device, stream: int):
+    """(job array, workspace, device info tensor) for kfac_invert_phase on `stream`."""
+    arr = as_array(InvertJob, jobs)
+    need = lib().kfac_invert_workspace_bytes(arr, len(jobs))
+    ws = workspace.get(device, need, stream)
+    info = torch.empty(len(jobs), dtype=torch.int32, device=device)
+    return arr, ws, info
+
+
+def invert_phase(arr, ws: torch.Tensor, info: torch.Tensor, phase: int, stream: int) -> None:
+    """kfac_invert_phase (ctypes releases the GIL for the call: safe from a worker thread)."""
+    check(lib().kfac_invert_phase(arr, len(arr), ws.data_ptr(), ws.numel(), info.data_ptr(), phase, stream),
+          "kfac_invert_phase")
 
 
 def cu_count(device: torch.device) -> int:

@@ -75,9 +75,7 @@ extern "C" size_t kfac_invert_workspace_bytes(const kfac_invert_job* jobs, int n
   return tot;
 }
 
-extern "C" int kfac_invert_ex(const kfac_invert_job* jobs, int njobs, void* workspace,
-                              size_t workspace_bytes, int32_t* info, void* inputs_read,
-                              kfac_stream_t stream) {
+static int check_jobs(const kfac_invert_job* jobs, int njobs) {
   if (njobs <= 0 || !jobs) return KFAC_EINVAL;
   for (int i = 0; i < njobs; ++i) {
     const kfac_invert_job& j = jobs[i];
@@ -86,22 +84,48 @@ extern "C" int kfac_invert_ex(const kfac_invert_job* jobs, int njobs, void* work
       return KFAC_EINVAL;
     if (j.n > 65536) return KFAC_EINVAL;
   }
-  if (workspace_bytes < kfac_invert_workspace_bytes(jobs, njobs)) return KFAC_EWORKSPACE;
-  ProfScope ps(KFAC_PROF_INVERT, (hipStream_t)stream);
+  return KFAC_OK;
+}
+
+// phase 0: every group's F-reading launch; phase 1: the rest
+static int invert_phase(const kfac_invert_job* jobs, int njobs, void* workspace, int32_t* info,
+                        hipStream_t stream, int phase) {
   const bool small = small_tiles(jobs, njobs);
   constexpr int IMAXJ = t64::IMAXJ;
   static_assert(t32::IMAXJ == t64::IMAXJ, "group size");
+  char* ws = (char*)workspace;
+  for (int g = 0; g < njobs; g += IMAXJ) {
+    const int ng = std::min(IMAXJ, njobs - g);
+    int32_t* inf = info ? info + g : nullptr;
+    const int rc = small ? t32::invert_group(jobs + g, ng, ws, inf, stream, phase)
+                         : t64::invert_group(jobs + g, ng, ws, inf, stream, phase);
+    if (rc) return rc;
+    for (int i = g; i < g + ng; ++i) ws += job_ws(jobs[i], small);
+  }
+  return KFAC_OK;
+}
+
+extern "C" int kfac_invert_phase(const kfac_invert_job* jobs, int njobs, void* workspace,
+                                 size_t workspace_bytes, int32_t* info, int phase, kfac_stream_t stream) {
+  const int rc = check_jobs(jobs, njobs);
+  if (rc) return rc;
+  if (phase != 0 && phase != 1) return KFAC_EINVAL;
+  if (workspace_bytes < kfac_invert_workspace_bytes(jobs, njobs)) return KFAC_EWORKSPACE;
+  ProfScope ps(KFAC_PROF_INVERT, (hipStream_t)stream);
+  return invert_phase(jobs, njobs, workspace, info, (hipStream_t)stream, phase);
+}
+
+extern "C" int kfac_invert_ex(const kfac_invert_job* jobs, int njobs, void* workspace,
+                              size_t workspace_bytes, int32_t* info, void* inputs_read,
+                              kfac_stream_t stream) {
+  const int rc0 = check_jobs(jobs, njobs);
+  if (rc0) return rc0;
+  if (workspace_bytes < kfac_invert_workspace_bytes(jobs, njobs)) return KFAC_EWORKSPACE;
+  ProfScope ps(KFAC_PROF_INVERT, (hipStream_t)stream);
   // every group's F-reading launch first, then the event, then the rest
   for (int phase = 0; phase < 2; ++phase) {
-    char* ws = (char*)workspace;
-    for (int g = 0; g < njobs; g += IMAXJ) {
-      const int ng = std::min(IMAXJ, njobs - g);
-      int32_t* inf = info ? info + g : nullptr;
-      const int rc = small ? t32::invert_group(jobs + g, ng, ws, inf, (hipStream_t)stream, phase)
-                           : t64::invert_group(jobs + g, ng, ws, inf, (hipStream_t)stream, phase);
-      if (rc) return rc;
-      for (int i = g; i < g + ng; ++i) ws += job_ws(jobs[i], small);
-    }
+    const int rc = invert_phase(jobs, njobs, workspace, info, (hipStream_t)stream, phase);
+    if (rc) return rc;
     if (phase == 0 && inputs_read &&
         hipEventRecord((hipEvent_t)inputs_read, (hipStream_t)stream) != hipSuccess)
       return KFAC_ELAUNCH;

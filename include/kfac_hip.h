@@ -159,6 +159,12 @@ KFAC_API int kfac_invert(const kfac_invert_job* jobs, int njobs, void* workspace
  * kfac_invert.                                                               */
 KFAC_API int kfac_invert_ex(const kfac_invert_job* jobs, int njobs, void* workspace,
                    size_t workspace_bytes, int32_t* info, void* inputs_read, kfac_stream_t stream);
+/* kfac_invert_ex in two calls: phase 0 = the launches that read F (the caller may
+ * record its own "inputs read" event after it), phase 1 = the rest, on the same
+ * stream, possibly from another host thread (KFAC.invert issues phase 1 from a
+ * worker thread so its ~25 step launches do not hold up the next data pass). */
+KFAC_API int kfac_invert_phase(const kfac_invert_job* jobs, int njobs, void* workspace,
+                               size_t workspace_bytes, int32_t* info, int phase, kfac_stream_t stream);
 /* Single-factor convenience: KFAC.invert for one factor. */
 KFAC_API int kfac_damped_inv_chol(const float* F, int n, int64_t ldF, double sqrt_s, double sqrt_n,
                          float* L, int64_t ldL, void* workspace, size_t workspace_bytes,
