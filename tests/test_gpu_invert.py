@@ -123,8 +123,9 @@ def test_singular_raises_linalgerror(hip_device):
         _ = kfac.inv_state  # ... and settled at the next inv_state read
     assert net[0] not in kfac.inv_state
     kfac.invert(0.0, 1.0)
+    torch.cuda.synchronize()  # the verdict is back before the next invert() starts ...
     with pytest.raises(np.linalg.LinAlgError):
-        kfac.invert(1.0, 1.0)  # or at the start of the next invert() (which then does not run)
+        kfac.invert(1.0, 1.0)  # ... so that invert() reads it and raises (and does not run)
     kfac.invert(1.0, 1.0)
     assert net[0] in kfac.inv_state
 
