@@ -702,10 +702,18 @@ class KFAC(Curvature):
         return s
 
     def _side_stream(self, device):
+        """The side stream of this inversion: two high-priority streams taken in turn,
+        each with its own workspace (the library's workspace cache is per stream), so
+        an inversion's F-reading launch does not queue behind the previous
+        inversion's steps: the next data pass waits only for the factors to be read."""
         s = self._inv_streams.get(device.index)
         if s is None:
-            s = self._inv_streams[device.index] = torch.cuda.Stream(device=device, priority=-1)
-        return s
+            s = self._inv_streams[device.index] = [torch.cuda.Stream(device=device, priority=-1)
+                                                   for _ in range(2)]
+        if not isinstance(s, list):  # a single stream set by hand (tools/probe_*.py)
+            return s
+        self._inv_turn = getattr(self, "_inv_turn", 0) ^ 1
+        return s[self._inv_turn]
 
     def _order_after(self, pending):
         """Later work on the caller's stream sees the inversion's factors, and the
@@ -718,16 +726,19 @@ class KFAC(Curvature):
                 t.record_stream(cur)
 
     def _defer_verdict(self):
-        """invert(): queue the pending inversion's verdict instead of waiting for it;
-        read the verdicts that are already back (at most 2 stay queued)."""
+        """invert(): queue the pending inversion's verdict instead of waiting for it,
+        and read the verdicts that are already back (at most 2 stay queued).  Queued
+        inversions are ordered before the caller's stream only when `inv_state` is
+        read (_check_inverse), so the next data pass does not wait for them."""
         pending = getattr(self, "_inv_pending", None)
         if pending is not None:
             self._inv_pending = None
-            self._order_after(pending)
             self._inv_older.append(pending)
         while self._inv_older and (len(self._inv_older) > 2 or
                                    self._joined(self._inv_older[0])[0].query()):
-            self._verdict(self._inv_older.pop(0))
+            p = self._inv_older.pop(0)
+            self._order_after(p)
+            self._verdict(p)
 
     def _check_inverse(self):
         """Settle every pending inversion, oldest first: a factor that is not positive
@@ -736,7 +747,9 @@ class KFAC(Curvature):
         dropped from `inv_state` as the reference never assigns them."""
         older = getattr(self, "_inv_older", [])
         while older:
-            self._verdict(older.pop(0))
+            p = older.pop(0)
+            self._order_after(p)
+            self._verdict(p)
         pending = getattr(self, "_inv_pending", None)
         if pending is None:
             return
