@@ -56,6 +56,12 @@ class QuadJob(ctypes.Structure):
                 ("lower2", c_i32), ("v", c_vp)]
 
 
+class SampleJob(ctypes.Structure):
+    _fields_ = [("LA", c_vp), ("ldA", c_i64), ("LG", c_vp), ("ldG", c_i64), ("Z", c_vp),
+                ("nA", c_i32), ("nG", c_i32), ("W", c_vp), ("ldW", c_i64), ("bias", c_vp),
+                ("wcols", c_i32), ("reserved", c_i32)]
+
+
 # symbol -> (restype, argtypes); every symbol include/kfac_hip.h declares
 SIGNATURES = {
     "kfac_factor_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(FactorJob), ctypes.c_int]),
@@ -85,6 +91,9 @@ SIGNATURES = {
                                                         c_i64]),
     "kfac_kron_quadform": (ctypes.c_int, [ctypes.POINTER(QuadJob), ctypes.c_int, c_i64,
                                           ctypes.c_int, c_vp, c_vp, ctypes.c_size_t, c_vp]),
+    "kfac_sample_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(SampleJob), ctypes.c_int]),
+    "kfac_sample": (ctypes.c_int, [ctypes.POINTER(SampleJob), ctypes.c_int, ctypes.c_int, c_vp,
+                                   ctypes.c_size_t, c_vp]),
     "kfac_invert_phase": (ctypes.c_int, [ctypes.POINTER(InvertJob), ctypes.c_int, c_vp, ctypes.c_size_t,
                                          c_vp, ctypes.c_int, c_vp]),
     "kfac_cu_count": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
@@ -307,6 +316,35 @@ def kron_quadform(jobs, nb: int, abs_sum: bool, out: torch.Tensor):
     ws = workspace.get(out.device, need)
     check(L.kfac_kron_quadform(arr, len(jobs), nb, int(abs_sum), ptr(out), ptr(ws), ws.numel(),
                                stream_handle(out.device)), "kfac_kron_quadform")
+
+
+def sample(jobs, device: torch.device, accumulate: bool) -> None:
+    """kfac_sample, <= 8 jobs per launch pair (KFAC.sample / sample_and_replace)."""
+    L = lib()
+    for i in range(0, len(jobs), 8):
+        chunk = jobs[i:i + 8]
+        arr = as_array(SampleJob, chunk)
+        ws = workspace.get(device, L.kfac_sample_workspace_bytes(arr, len(chunk)))
+        check(L.kfac_sample(arr, len(chunk), int(accumulate), ptr(ws), ws.numel(),
+                            stream_handle(device)), "kfac_sample")
+
+
+def sample_job(LA: torch.Tensor, LG: torch.Tensor, z: torch.Tensor, W: torch.Tensor, wcols: int,
+               bias: torch.Tensor = None) -> SampleJob:
+    """(LA z LG^T)^T into W (nG rows, columns < wcols) and, when wcols == nA - 1, its
+    last column into bias."""
+    for t in (LA, LG, z, W) + ((bias,) if bias is not None else ()):
+        require_device(t, "sample operand")
+        if t.stride(-1) != 1:
+            raise NativeError("sample operands need a unit column stride")
+    nA, nG = LA.shape[0], LG.shape[0]
+    if tuple(z.shape) != (nA, nG) or not z.is_contiguous():
+        raise NativeError(f"sample: z must be a contiguous ({nA}, {nG}) tensor")
+    if W.dim() != 2 or W.shape[0] != nG or W.shape[1] < wcols:
+        raise NativeError(f"sample: output must be ({nG}, >= {wcols})")
+    return SampleJob(LA.data_ptr(), LA.stride(0), LG.data_ptr(), LG.stride(0), z.data_ptr(), nA, nG,
+                     W.data_ptr(), W.stride(0), bias.data_ptr() if bias is not None else None,
+                     wcols, 0)
 
 
 # ---------------------------------------------------------------- job builders

@@ -603,8 +603,15 @@ class KFAC(Curvature):
         # one-launch-per-step range, <= 24 tiles of 64): a large factor's inversion is
         # throughput-bound and needs the whole chip (wide MLP, 4097^2: 4x slower on 32 CUs)
         part = self._partition(device) if self.overlap_invert else None
-        part_side = part is not None and max(F_.shape[0] for _, v in entries for F_ in v) <= 24 * 64
-        side = (part[1] if part_side else self._side_stream(device)) if self.overlap_invert else main
+        latency_bound = max(F_.shape[0] for _, v in entries for F_ in v) <= 24 * 64
+        part_side = part is not None and latency_bound
+        side = ((part[1] if part_side else self._side_stream(device, alternate=latency_bound))
+                if self.overlap_invert else main)
+        if not latency_bound:
+            # same stream and workspace as the previous inversion: its worker-issued
+            # launches must be queued before this one's first launch overwrites it
+            for p in getattr(self, "_inv_older", []):
+                self._joined(p)
         read = None
         if side is not main:
             side.wait_stream(main)
@@ -701,17 +708,22 @@ class KFAC(Curvature):
             s = self._copy_streams[device.index] = torch.cuda.Stream(device=device)
         return s
 
-    def _side_stream(self, device):
+    def _side_stream(self, device, alternate=True):
         """The side stream of this inversion: two high-priority streams taken in turn,
         each with its own workspace (the library's workspace cache is per stream), so
         an inversion's F-reading launch does not queue behind the previous
-        inversion's steps: the next data pass waits only for the factors to be read."""
+        inversion's steps: the next data pass waits only for the factors to be read.
+        A throughput-bound inversion (`alternate` False: some factor > 24 tiles of 64)
+        always takes the first stream, so two of them never run at once and split the
+        chip (wide MLP: 13.8 -> 25.5 ms per inversion when they did)."""
         s = self._inv_streams.get(device.index)
         if s is None:
             s = self._inv_streams[device.index] = [torch.cuda.Stream(device=device, priority=-1)
                                                    for _ in range(2)]
         if not isinstance(s, list):  # a single stream set by hand (tools/probe_*.py)
             return s
+        if not alternate:
+            return s[0]
         self._inv_turn = getattr(self, "_inv_turn", 0) ^ 1
         return s[self._inv_turn]
 
@@ -781,4 +793,36 @@ class KFAC(Curvature):
         assert self.inv_state, "Inverse state dict is empty. Did you call 'invert' prior to this?"
         first, second = self.inv_state[layer]
         z = torch.randn(first.size(0), second.size(0), device=first.device, dtype=first.dtype)
-        return (first @ z @ second.t()).t()
+        out = torch.empty(second.size(0), first.size(0), device=first.device, dtype=first.dtype)
+        N.sample([N.sample_job(first, second, z, out, first.size(0))], first.device, accumulate=False)
+        return out
+
+    def sample_and_replace(self):
+        """Curvature.sample_and_replace (curvatures.py:117-129) in one launch pair: the
+        mean weights are restored, then every layer's (L_A z L_G^T)^T is added into its
+        weight rows and bias (Curvature._replace, curvatures.py:68-82) by kfac_sample.
+        z is drawn per layer in model.modules() order, as the reference draws it."""
+        inv_state = self.inv_state
+        assert inv_state, "Inverse state dict is empty. Did you call 'invert' prior to this?"
+        self.model.load_state_dict(self.model_state)
+        # the draws stay referenced until the launch is queued (a freed z would be
+        # handed to the next draw by the caching allocator)
+        jobs, draws, device = [], [], None
+        for layer in self.model.modules():
+            if layer.__class__.__name__ not in self.layer_types:
+                continue
+            if layer.__class__.__name__ not in ['Linear', 'Conv2d']:
+                continue
+            first, second = inv_state[layer]
+            nA, nG = first.size(0), second.size(0)
+            z = torch.randn(nA, nG, device=first.device, dtype=first.dtype)
+            draws.append(z)
+            weight, bias = layer.weight.data, layer.bias.data if layer.bias is not None else None
+            wcols = nA - 1 if bias is not None else nA
+            if not weight.is_contiguous() or weight.numel() != nG * wcols:
+                raise N.NativeError(f"sample_and_replace: {layer} weight is not a contiguous "
+                                    f"({nG} x {wcols}) block")
+            jobs.append(N.sample_job(first, second, z, weight.view(nG, wcols), wcols, bias))
+            device = first.device
+        if jobs:
+            N.sample(jobs, device, accumulate=True)

@@ -212,6 +212,32 @@ KFAC_API size_t kfac_quadform_workspace_bytes(const kfac_quad_job* jobs, int njo
 KFAC_API int kfac_kron_quadform(const kfac_quad_job* jobs, int njobs, int64_t nb, int abs_sum, float* out,
                        void* workspace, size_t workspace_bytes, kfac_stream_t stream);
 
+/* -------------------------------------------------------- posterior samples
+ * out_j = (LA_j Z_j LG_j^T)^T, shape (nG x nA): KFAC.sample, curvatures.py:400-405,
+ * with Z (nA x nG row-major) supplied by the caller (torch.randn, the reference's
+ * draw).  LA/LG are lower-triangular with zero upper triangles (KFAC.invert's
+ * factors): tiles above the diagonal are skipped.  Columns a < wcols go to W[g*ldW + a]; when wcols == nA-1 column
+ * nA-1 goes to bias[g] (Curvature._replace, curvatures.py:68-82; bias may be NULL
+ * to drop it).  accumulate: W += sample (sample_and_replace) else W = sample.
+ * At most 8 jobs per call.                                                    */
+typedef struct kfac_sample_job {
+  const float* LA;
+  int64_t ldA;
+  const float* LG;
+  int64_t ldG;
+  const float* Z;
+  int32_t nA, nG;
+  float* W;
+  int64_t ldW;
+  float* bias;
+  int32_t wcols;
+  int32_t reserved;
+} kfac_sample_job;
+
+KFAC_API size_t kfac_sample_workspace_bytes(const kfac_sample_job* jobs, int njobs);
+KFAC_API int kfac_sample(const kfac_sample_job* jobs, int njobs, int accumulate, void* workspace,
+                size_t workspace_bytes, kfac_stream_t stream);
+
 /* -------------------------------------------------------------- profiling
  * Optional HIP-event timing of the library's own launches, recorded on the
  * stream each kernel is launched on (off by default; not graph-capturable when

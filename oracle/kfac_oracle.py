@@ -172,6 +172,24 @@ def kron(a, b) -> np.ndarray:
     return np.einsum("ab,cd->acbd", a, b).reshape(a.shape[0] * b.shape[0], a.shape[1] * b.shape[1])
 
 
+# ------------------------------------------------------------------ posterior samples
+def sample(LA, LG, z, dtype=np.float64) -> np.ndarray:
+    """models/curvatures.py:400-405: (L_A @ z @ L_G^T)^T, shape (n_G, n_A); z is the
+    caller's N(0, 1) draw of shape (n_A, n_G)."""
+    LA, LG, z = (np.asarray(t, dtype=dtype) for t in (LA, LG, z))
+    return (LA @ z @ LG.T).T
+
+
+def replace(sample_, weight, bias=None):
+    """models/curvatures.py:68-82 (Curvature._replace), out of place: the last column
+    of the sample goes to the bias, the rest (reshaped) to the weight."""
+    weight = np.asarray(weight)
+    if bias is not None:
+        bias = np.asarray(bias) + sample_[:, -1].reshape(np.shape(bias))
+        sample_ = sample_[:, :-1]
+    return weight + sample_.reshape(weight.shape), bias
+
+
 # -------------------------------------------------------------- predictive variance
 def kron_quadform(J: np.ndarray, K1: np.ndarray, K2: np.ndarray, dtype=np.float64) -> np.ndarray:
     """v_b = J_b kron(K1, K2) J_b^T for each row b of J, without forming the kron.

@@ -20,6 +20,8 @@ exercised are:
   predictive-variance loop (no CUDA guard, as in the noise loop) (G6)
 * `sampling_free/regression/regression_ll_block.py:102-140`  regression
   `pinv(N(q+tau I)) (x) pinv(N(h+tau I))` quadratic form (G7)
+* `models/curvatures.py:400-405, 117-129, 68-82`  KFAC.sample, sample_and_replace and
+  Curvature._replace on a conv (bias) + linear (no bias) net, with the z draws (G8)
 """
 import os
 import sys
@@ -316,6 +318,42 @@ def g7_regression():
     save("g7_regression.npz", **out)
 
 
+# ------------------------------------- G8 posterior samples (sample / sample_and_replace)
+def g8_sample():
+    """curvatures.py:400-405 + 117-129 + 68-82 on a conv (bias) + linear (no bias) net:
+    the reference's z draws, its samples and the replaced weights."""
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Conv2d(2, 3, 3), nn.Flatten(), nn.Linear(48, 5, bias=False))
+    kfac = KFAC(net)
+    rng = np.random.default_rng(8)
+    x = rng.random((7, 2, 6, 6), dtype=np.float32)
+    gc = rng.standard_normal((7, 3, 4, 4), dtype=np.float32)
+    a = rng.random((7, 48), dtype=np.float32)
+    gl = rng.standard_normal((7, 5), dtype=np.float32)
+    inject_update(kfac, [net[0], net[2]], [(torch.from_numpy(x), torch.from_numpy(gc)),
+                                         (torch.from_numpy(a), torch.from_numpy(gl))], 7)
+    kfac.invert(0.04, 200)
+    res = {}
+    for i, layer in ((0, net[0]), (2, net[2])):
+        LA, LG = kfac.inv_state[layer]
+        res[f"LA{i}"], res[f"LG{i}"] = npf(LA), npf(LG)
+        res[f"W{i}_mean"] = npf(layer.weight)
+    res["b0_mean"] = npf(net[0].bias)
+    # kfac.sample(layer): one draw
+    torch.manual_seed(11)
+    res["sample2"] = npf(kfac.sample(net[2]))
+    torch.manual_seed(11)
+    res["z_sample2"] = npf(torch.randn(res["LA2"].shape[0], res["LG2"].shape[0]))
+    # sample_and_replace: one draw per layer, modules() order
+    torch.manual_seed(12)
+    kfac.sample_and_replace()
+    res["W0_new"], res["b0_new"], res["W2_new"] = npf(net[0].weight), npf(net[0].bias), npf(net[2].weight)
+    torch.manual_seed(12)
+    res["z0"] = npf(torch.randn(res["LA0"].shape[0], res["LG0"].shape[0]))
+    res["z2"] = npf(torch.randn(res["LA2"].shape[0], res["LG2"].shape[0]))
+    save("g8_sample.npz", **res)
+
+
 if __name__ == "__main__":
     g0_kron()
     g1_small_linear()
@@ -324,3 +362,4 @@ if __name__ == "__main__":
     g4_conv()
     g5_g6_basenet()
     g7_regression()
+    g8_sample()

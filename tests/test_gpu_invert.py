@@ -266,3 +266,26 @@ def test_cu_partitioned_passes_match_serial(hip_device):
             R = O.damped_factor(F.astype(np.float64), 0.04, 200)
             Ld = L.astype(np.float64)
             assert np.abs(Ld.T @ R @ Ld - np.eye(R.shape[0])).max() < 1e-3
+
+
+def test_back_to_back_throughput_bound_inversions(hip_device):
+    """A factor > 24 tiles of 64 (here 1601^2) takes the single side stream: inversions
+    queued back to back share its workspace, so each must be fully queued before the
+    next starts (wide-MLP bench regression: spurious LinAlgError)."""
+    import torch.nn as nn
+    from bnn_kfac_amd.curvatures import KFAC
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Linear(1600, 8)).to(hip_device)
+    kfac = KFAC(net)
+    x = torch.rand(512, 1600, device=hip_device)
+    for _ in range(4):
+        net.zero_grad()
+        nn.functional.cross_entropy(net(x), torch.randint(0, 8, (512,), device=hip_device)).backward()
+        kfac.update(batch_size=512)
+        kfac.invert(0.04, 200)
+    LA, LG = kfac.inv_state[net[0]]
+    A = kfac.state[net[0]][0].double()
+    R = (200 ** 0.5) * A + (0.04 ** 0.5) * torch.eye(A.shape[0], device=hip_device, dtype=torch.float64)
+    L = LA.double()
+    err = (L.t() @ R @ L - torch.eye(A.shape[0], device=hip_device, dtype=torch.float64)).abs().max()
+    assert err < 1e-3, float(err)

@@ -67,3 +67,19 @@ def test_workspace_queries_need_no_gpu():
     # argument validation happens before any launch
     bad = N.FactorJob()
     assert lib.kfac_factor_update(N.as_array(N.FactorJob, [bad]), 1, None, 0, None) == N.KFAC_EINVAL
+
+
+def test_sample_struct_layout(tmp_path):
+    from bnn_kfac_amd import _native as N
+    c = tmp_path / "sz.c"
+    c.write_text(f'#include <stdio.h>\n#include <stddef.h>\n#include "{HEADER}"\n'
+                 'int main(void){printf("%zu %zu %zu", sizeof(kfac_sample_job), '
+                 'offsetof(kfac_sample_job, W), offsetof(kfac_sample_job, wcols)); return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-o", str(exe), str(c)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    assert got == [ctypes.sizeof(N.SampleJob), N.SampleJob.W.offset, N.SampleJob.wcols.offset]
+    # argument validation happens before any launch
+    assert N.lib().kfac_sample(N.as_array(N.SampleJob, [N.SampleJob()]), 1, 0, None, 0,
+                               None) == N.KFAC_EWORKSPACE

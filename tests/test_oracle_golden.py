@@ -160,3 +160,16 @@ def test_regression_quadform():
             np.testing.assert_allclose(v, g["v"][j, li], rtol=2e-3, atol=1e-7)
             std_j += abs(v)
         np.testing.assert_allclose(std_j ** 0.5 + sigma, g["std"][j], rtol=1e-4)
+
+
+def test_sample_and_replace_golden():
+    """G8: the oracle's sample / _replace against the reference's own draws
+    (curvatures.py:400-405, 117-129, 68-82)."""
+    g = golden("g8_sample.npz")
+    s2 = O.sample(g["LA2"], g["LG2"], g["z_sample2"])
+    np.testing.assert_allclose(s2, g["sample2"], rtol=1e-5, atol=1e-6 * np.abs(s2).max())
+    s0 = O.sample(g["LA0"], g["LG0"], g["z0"])
+    W0, b0 = O.replace(s0, g["W0_mean"], g["b0_mean"])
+    W2, _ = O.replace(O.sample(g["LA2"], g["LG2"], g["z2"]), g["W2_mean"])
+    for got, want in ((W0, g["W0_new"]), (b0, g["b0_new"]), (W2, g["W2_new"])):
+        np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-6)
