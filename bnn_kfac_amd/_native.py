@@ -59,7 +59,7 @@ class QuadJob(ctypes.Structure):
 class SampleJob(ctypes.Structure):
     _fields_ = [("LA", c_vp), ("ldA", c_i64), ("LG", c_vp), ("ldG", c_i64), ("Z", c_vp),
                 ("nA", c_i32), ("nG", c_i32), ("W", c_vp), ("ldW", c_i64), ("bias", c_vp),
-                ("wcols", c_i32), ("reserved", c_i32)]
+                ("wcols", c_i32), ("dense", c_i32)]
 
 
 # symbol -> (restype, argtypes); every symbol include/kfac_hip.h declares
@@ -330,7 +330,7 @@ def sample(jobs, device: torch.device, accumulate: bool) -> None:
 
 
 def sample_job(LA: torch.Tensor, LG: torch.Tensor, z: torch.Tensor, W: torch.Tensor, wcols: int,
-               bias: torch.Tensor = None) -> SampleJob:
+               bias: torch.Tensor = None, dense: bool = False) -> SampleJob:
     """(LA z LG^T)^T into W (nG rows, columns < wcols) and, when wcols == nA - 1, its
     last column into bias."""
     for t in (LA, LG, z, W) + ((bias,) if bias is not None else ()):
@@ -344,7 +344,7 @@ def sample_job(LA: torch.Tensor, LG: torch.Tensor, z: torch.Tensor, W: torch.Ten
         raise NativeError(f"sample: output must be ({nG}, >= {wcols})")
     return SampleJob(LA.data_ptr(), LA.stride(0), LG.data_ptr(), LG.stride(0), z.data_ptr(), nA, nG,
                      W.data_ptr(), W.stride(0), bias.data_ptr() if bias is not None else None,
-                     wcols, 0)
+                     wcols, int(dense))
 
 
 # ---------------------------------------------------------------- job builders

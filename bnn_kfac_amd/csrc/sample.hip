@@ -10,8 +10,10 @@
 //   1. Y = L_A z                  (nA x nG)   Y[a][j] = sum_{i <= a} L_A[a][i] z[i][j]
 //   2. out[g][a] (+)= sum_{j <= g} L_G[g][j] Y[a][j]   = (L_A z L_G^T)^T
 // Both factors are lower-triangular (KFAC.invert's Cholesky factors), so each tile
-// contracts only the K-range its triangle leaves non-zero.  Launch 2's output tile is
-// indexed (g, a) so the MFMA lanes walk a: weight rows are written coalesced.  z is
+// contracts only the K-range its triangle leaves non-zero; `dense` jobs (EFB.sample,
+// curvatures.py:466-473: eigenvector matrices, z pre-scaled by the host) contract
+// all of K.  Launch 2's output tile is indexed (g, a) so the MFMA lanes walk a:
+// weight rows are written coalesced.  z is
 // the caller's (torch.randn in the reference's order), so samples match the
 // reference draw for draw.
 #include "kfac_common.h"
@@ -27,7 +29,7 @@ struct SampleJobDev {
   float* W;
   float* bias;
   int64_t ldW;
-  int nA, nG, wcols, accumulate;
+  int nA, nG, wcols, accumulate, dense;
   int t1_begin, t2_begin;  // first task of this job in launch 1 / launch 2
 };
 
@@ -56,8 +58,8 @@ __global__ __launch_bounds__(NTHREADS) void kfac_sample_ly(SampleArgs args) {
   floatx16 acc;
 #pragma unroll
   for (int v = 0; v < 16; ++v) acc[v] = 0.f;
-  // L_A lower: L_A[a][i] = 0 for i > a, so i < a0 + 64 suffices
-  const int64_t kend = min((int64_t)S.nA, (int64_t)a0 + TILE);
+  // L_A lower: L_A[a][i] = 0 for i > a, so i < a0 + 64 suffices (dense: all i)
+  const int64_t kend = S.dense ? (int64_t)S.nA : min((int64_t)S.nA, (int64_t)a0 + TILE);
   contract_tile<KFAC_CHANNEL, KFAC_ROWMAJOR>(S.la_t, a0, S.z, j0, 0, kend, false, true, lds, acc);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = j0 + (wave & 1) * 32 + (lane & 31);
@@ -82,8 +84,8 @@ __global__ __launch_bounds__(NTHREADS) void kfac_sample_out(SampleArgs args) {
   floatx16 acc;
 #pragma unroll
   for (int v = 0; v < 16; ++v) acc[v] = 0.f;
-  // L_G lower: j <= g, so j < g0 + 64 suffices
-  const int64_t kend = min((int64_t)S.nG, (int64_t)g0 + TILE);
+  // L_G lower: j <= g, so j < g0 + 64 suffices (dense: all j)
+  const int64_t kend = S.dense ? (int64_t)S.nG : min((int64_t)S.nG, (int64_t)g0 + TILE);
   contract_tile<KFAC_CHANNEL, KFAC_CHANNEL>(S.lg_t, g0, S.y_t, a0, 0, kend, false, true, lds, acc);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int a = a0 + (wave & 1) * 32 + (lane & 31);
@@ -136,6 +138,7 @@ extern "C" int kfac_sample(const kfac_sample_job* jobs, int njobs, int accumulat
     d.nG = q.nG;
     d.wcols = q.wcols;
     d.accumulate = accumulate;
+    d.dense = q.dense != 0;
     // element (i, a) of L_A^T = LA[a*ldA + i]: CHANNEL with L = ldA (rows = K = nA)
     d.la_t = OpDev{};
     d.la_t.ptr = q.LA; d.la_t.layout = KFAC_CHANNEL; d.la_t.rows = q.nA; d.la_t.cols = q.nA;

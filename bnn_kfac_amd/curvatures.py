@@ -826,3 +826,68 @@ class KFAC(Curvature):
             device = first.device
         if jobs:
             N.sample(jobs, device, accumulate=True)
+
+
+class EFB(Curvature):
+    r"""Eigenvalue-corrected Kronecker factorisation (models/curvatures.py:408-470).
+
+    The eigenbases of the KFAC factors come from the device eigensolver
+    (`utilities.get_eigenvectors` -> kfac_syev; the reference's `torch.symeig` no longer
+    exists on torch >= 2.0).  `update` projects each layer's batch gradient into the
+    eigenbasis, lambda = (V_G^T grad V_A)^2 (two plain device GEMMs, rocBLAS via torch)
+    and accumulates it; `sample` draws z * lambda^{-1/2} and maps it back through the
+    eigenbases with kfac_sample (dense factors).
+    """
+
+    def __init__(self, model: Union[Module, Sequential], factors, layer_types: Union[List[str], str] = None):
+        super().__init__(model, layer_types)
+        from .utilities import get_eigenvectors
+        self.eigvecs = get_eigenvectors(factors)
+        self.diags = dict()
+
+    def update(self, batch_size: int):
+        """curvatures.py:427-449: state += (V_G^T grad V_A)^2, diags += grad^2 * B."""
+        for layer in self.model.modules():
+            if layer.__class__.__name__ in self.layer_types:
+                if layer.__class__.__name__ in ['Linear', 'Conv2d']:
+                    grads = layer.weight.grad.contiguous().view(layer.weight.grad.shape[0], -1)
+                    if layer.bias is not None:
+                        grads = torch.cat([grads, layer.bias.grad.unsqueeze(dim=1)], dim=1)
+                    N.require_device(grads, "weight grad", layer)
+                    V_A, V_G = self.eigvecs[layer]
+                    lambdas = (V_G.t() @ grads @ V_A) ** 2
+                    if layer in self._state:
+                        self._state[layer] += lambdas
+                        self.diags[layer] += grads ** 2 * batch_size
+                    else:
+                        self._state[layer] = lambdas
+                        self.diags[layer] = grads ** 2 * batch_size
+                elif layer.__class__.__name__ == 'MultiheadAttention':
+                    raise NotImplementedError
+
+    def invert(self, add: Union[float, list, tuple] = 0., multiply: Union[float, list, tuple] = 1.):
+        """curvatures.py:451-464: inv_state = (s * lambda + n)^{-1/2}, elementwise.  The
+        reference tests `isinstance(.., float)` here (not int): an int damping is treated
+        as a list and fails its length assert, as there."""
+        assert self.state, "State dict is empty. Did you call 'update' prior to this?"
+        if self.inv_state:
+            Warning("State has already been inverted. Is this expected?")
+        for index, (layer, value) in enumerate(self.state.items()):
+            if not isinstance(add, float) and not isinstance(multiply, float):
+                assert len(add) == len(multiply) == len(self.state)
+                n, s = add[index], multiply[index]
+            else:
+                n, s = add, multiply
+            self._inv_state[layer] = torch.reciprocal(s * value + n).sqrt()
+
+    def sample(self, layer: Module) -> Tensor:
+        """curvatures.py:466-473: (V_A (z * lambda^T) V_G^T)^T, z ~ N(0, 1)."""
+        assert self.inv_state, "Inverse state dict is empty. Did you call 'invert' prior to this?"
+        first, second = self.eigvecs[layer]
+        lambdas = self.inv_state[layer]
+        z = torch.randn(first.size(0), second.size(0), device=first.device, dtype=first.dtype)
+        z *= lambdas.t()
+        out = torch.empty(second.size(0), first.size(0), device=first.device, dtype=first.dtype)
+        N.sample([N.sample_job(first, second, z, out, first.size(0), dense=True)], first.device,
+                 accumulate=False)
+        return out

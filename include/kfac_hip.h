@@ -231,7 +231,7 @@ typedef struct kfac_sample_job {
   int64_t ldW;
   float* bias;
   int32_t wcols;
-  int32_t reserved;
+  int32_t dense; /* 1: LA/LG are full matrices (EFB eigenvectors, curvatures.py:466-473) */
 } kfac_sample_job;
 
 KFAC_API size_t kfac_sample_workspace_bytes(const kfac_sample_job* jobs, int njobs);

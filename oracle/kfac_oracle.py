@@ -190,6 +190,26 @@ def replace(sample_, weight, bias=None):
     return weight + sample_.reshape(weight.shape), bias
 
 
+# ------------------------------------------------------------------------------ EFB
+# The reference's EFB cannot run on torch >= 2.0 (get_eigenvectors calls the removed
+# torch.symeig), so these restatements are pinned by the reference's lines only.
+def efb_lambdas(grads, V_A, V_G, dtype=np.float64) -> np.ndarray:
+    """models/curvatures.py:436-440: (V_G^T grads V_A)^2, grads = [dW | db] (n_G x n_A)."""
+    grads, V_A, V_G = (np.asarray(t, dtype=dtype) for t in (grads, V_A, V_G))
+    return (V_G.T @ grads @ V_A) ** 2
+
+
+def efb_invert(lambdas, n, s, dtype=np.float64) -> np.ndarray:
+    """models/curvatures.py:461-462: (s * lambda + n)^{-1/2}."""
+    return 1.0 / np.sqrt(s * np.asarray(lambdas, dtype=dtype) + n)
+
+
+def efb_sample(V_A, V_G, inv_lambdas, z, dtype=np.float64) -> np.ndarray:
+    """models/curvatures.py:466-473: (V_A (z * inv_lambda^T) V_G^T)^T."""
+    V_A, V_G, il, z = (np.asarray(t, dtype=dtype) for t in (V_A, V_G, inv_lambdas, z))
+    return (V_A @ (z * il.T) @ V_G.T).T
+
+
 # -------------------------------------------------------------- predictive variance
 def kron_quadform(J: np.ndarray, K1: np.ndarray, K2: np.ndarray, dtype=np.float64) -> np.ndarray:
     """v_b = J_b kron(K1, K2) J_b^T for each row b of J, without forming the kron.

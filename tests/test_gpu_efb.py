@@ -1,0 +1,81 @@
+"""GPU: EFB (models/curvatures.py:408-473) on the device eigenbases against the fp64
+oracle.  The reference's EFB cannot run on torch >= 2.0 (torch.symeig is gone), so
+parity is pinned by the restatement of its lines (oracle.efb_*), not by a fixture.
+
+Tolerances: lambdas (squared projections onto the device's eigenbasis, itself checked
+orthonormal and diagonalising F + F^T) at rtol 1e-4 of the largest lambda; the sample is compared with the oracle on the
+device's eigenvectors at rtol 1e-5 of its magnitude."""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from oracle import kfac_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(dev):
+    from bnn_kfac_amd.curvatures import EFB, KFAC
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Conv2d(1, 3, 3), nn.ReLU(), nn.Flatten(), nn.Linear(3 * 6 * 6, 5)).to(dev)
+    kfac = KFAC(net)
+    grads = {m: [] for m in (net[0], net[3])}
+    for _ in range(2):
+        x = torch.rand(32, 1, 8, 8, device=dev)
+        net.zero_grad()
+        nn.functional.cross_entropy(net(x), torch.randint(0, 5, (32,), device=dev)).backward()
+        kfac.update(batch_size=32)
+    factors = {m: [F.clone() for F in v] for m, v in kfac.state.items()}
+    efb = EFB(net, factors)
+    for _ in range(3):
+        x = torch.rand(32, 1, 8, 8, device=dev)
+        net.zero_grad()
+        nn.functional.cross_entropy(net(x), torch.randint(0, 5, (32,), device=dev)).backward()
+        for m in grads:
+            g = m.weight.grad.reshape(m.weight.shape[0], -1)
+            grads[m].append(torch.cat([g, m.bias.grad[:, None]], 1).cpu().numpy())
+        efb.update(batch_size=32)
+    return net, factors, efb, grads
+
+
+def test_efb_update_invert_vs_oracle(hip_device):
+    net, factors, efb, grads = _setup(hip_device)
+    for m in (net[0], net[3]):
+        # the device basis (the Linear layer's A is rank-deficient: its null space has
+        # no unique basis); it must be an orthonormal eigenbasis of F + F^T
+        V_A, V_G = (v.cpu().numpy().astype(np.float64) for v in efb.eigvecs[m])
+        for F, V in zip(factors[m], (V_A, V_G)):
+            S = F.cpu().numpy().astype(np.float64)
+            S = S + S.T
+            np.testing.assert_allclose(V.T @ V, np.eye(len(V)), atol=1e-5)
+            D = V.T @ S @ V
+            assert np.abs(D - np.diag(np.diag(D))).max() < 1e-5 * np.abs(S).max()
+        want = sum(O.efb_lambdas(g, V_A, V_G) for g in grads[m])
+        got = efb.state[m].cpu().numpy()
+        np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-4 * want.max())
+        want_d = sum(g.astype(np.float64) ** 2 * 32 for g in grads[m])
+        np.testing.assert_allclose(efb.diags[m].cpu().numpy(), want_d, rtol=1e-5, atol=1e-9)
+    efb.invert(0.04, 200.0)
+    for m in (net[0], net[3]):
+        lam = efb.state[m].cpu().numpy()
+        np.testing.assert_allclose(efb.inv_state[m].cpu().numpy(), O.efb_invert(lam, 0.04, 200.0),
+                                   rtol=1e-5)
+    with pytest.raises(TypeError):  # int damping is taken as a list (curvatures.py:457-459)
+        efb.invert(0, 1)
+
+
+def test_efb_sample_vs_oracle(hip_device):
+    net, _, efb, _ = _setup(hip_device)
+    efb.invert(0.04, 200.0)
+    for m in (net[0], net[3]):
+        torch.manual_seed(5)
+        s = efb.sample(m).cpu().numpy()
+        V_A, V_G = (v.cpu().numpy() for v in efb.eigvecs[m])
+        torch.manual_seed(5)
+        z = torch.randn(V_A.shape[0], V_G.shape[0], device=hip_device).cpu().numpy()
+        want = O.efb_sample(V_A, V_G, efb.inv_state[m].cpu().numpy(), z)
+        np.testing.assert_allclose(s, want, rtol=1e-5, atol=1e-5 * np.abs(want).max())
+    before = net[3].weight.detach().clone()
+    efb.sample_and_replace()
+    assert not torch.equal(before, net[3].weight) and torch.isfinite(net[3].weight).all()
