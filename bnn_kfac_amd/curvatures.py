@@ -891,3 +891,116 @@ class EFB(Curvature):
         N.sample([N.sample_job(first, second, z, out, first.size(0), dense=True)], first.device,
                  accumulate=False)
         return out
+
+
+class INF(Curvature):
+    r"""Low-rank EFB + diagonal correction (models/curvatures.py:476-682) on the device.
+
+    `update(rank)` keeps the top-|lambda| eigenvector pairs (`_dim_reduction`, the
+    reference's 1-based index arithmetic restated in tensor form) and the diagonal
+    correction diag - sif_diag, where sif_diag (`_diagonal_accumulator`, a per-row loop
+    over kron products in the reference) is ONE GEMM chain: (V_A*V_A) Lambda (V_G*V_G)^T.
+    `invert` forms the pre-sample; V_s^T V_s is contracted without materialising the
+    (nA*nG x r) kron(U_A, U_G) the reference builds (`pre_sampler`, :545-580).
+    """
+
+    def __init__(self, model: Union[Module, Sequential], diags, factors, lambdas,
+                 layer_types: Union[List[str], str] = None):
+        super().__init__(model, layer_types)
+        assert diags.keys() == factors.keys() == lambdas.keys()
+        from .utilities import get_eigenvectors
+        self.eigvecs = get_eigenvectors(factors)
+        self.lambdas = lambdas
+        self.diags = diags
+
+    def update(self, rank: int = 100):
+        """curvatures.py:499-520."""
+        for layer, (xxt_eigvecs, ggt_eigvecs), lambdas, diags in zip(
+                list(self.diags.keys()), list(self.eigvecs.values()), list(self.lambdas.values()),
+                list(self.diags.values())):
+            N.require_device(lambdas, "lambdas", layer)
+            lambda_vec = lambdas.t().contiguous().view(-1)
+            diag_vec = diags.t().contiguous().view(-1)
+            lr_a, lr_g, lr_lambda = self._dim_reduction(xxt_eigvecs, ggt_eigvecs, lambda_vec, rank)
+            sif_diag = self._diagonal_accumulator(lr_a, lr_g, lr_lambda)
+            self._state[layer] = (lr_a, lr_g, lr_lambda, diag_vec - sif_diag)
+
+    def invert(self, add: Union[float, list, tuple] = 0., multiply: Union[float, list, tuple] = 1.):
+        """curvatures.py:522-540 (float damping or lists, as the reference tests it)."""
+        assert self.state, "State dict is empty. Did you call 'update' prior to this?"
+        if self.inv_state:
+            Warning("State has already been inverted. Is this expected?")
+        for index, (layer, value) in enumerate(self.state.items()):
+            if not isinstance(add, float) and not isinstance(multiply, float):
+                assert len(add) == len(multiply) == len(self.state)
+                n, s = add[index], multiply[index]
+            else:
+                n, s = add, multiply
+            lr_a, lr_g, lr_lambda, correction = value
+            correction[correction < 0] = 0
+            reg_lr_lambda = (s * lr_lambda).sqrt()
+            reg_inv_correction = torch.reciprocal(s * correction + n).sqrt()
+            pre_sample = self.pre_sampler(lr_a, lr_g, reg_lr_lambda, reg_inv_correction)
+            self._inv_state[layer] = (lr_a, lr_g, reg_inv_correction, pre_sample)
+
+    def sample(self, layer: Module) -> Tensor:
+        """curvatures.py:542-546."""
+        assert self.inv_state, "Inverse state dict is empty. Did you call 'invert' prior to this?"
+        a, b, c, d = self.inv_state[layer]
+        return self.sampler(a, b, c, d).reshape(a.shape[0], b.shape[0]).t()
+
+    @staticmethod
+    def pre_sampler(frst_eigvecs: Tensor, scnd_eigvecs: Tensor, reg_lambda: Tensor,
+                    reg_inv_correction: Tensor) -> Tensor:
+        """curvatures.py:548-580.  V_s = c * kron(U_A, U_G) diag(sigma) is never formed:
+        (V_s^T V_s)[(p,q),(p',q')] = sigma sigma' sum_a U_A[a,p] U_A[a,p'] T[a,q,q'],
+        T[a] = U_G^T diag(c[a,:]^2) U_G."""
+        nA, la = frst_eigvecs.shape
+        nG, lg = scnd_eigvecs.shape
+        c2 = (reg_inv_correction.view(nA, nG) ** 2)
+        T = torch.einsum('ag,gq,gQ->aqQ', c2, scnd_eigvecs, scnd_eigvecs)
+        vtv = torch.einsum('ap,aP,aqQ->pqPQ', frst_eigvecs, frst_eigvecs, T).reshape(la * lg, la * lg)
+        vtv = reg_lambda[:, None] * vtv * reg_lambda[None, :]
+        vtv = (vtv + vtv.t()) / 2.
+        eye = torch.eye(vtv.shape[0], device=vtv.device, dtype=vtv.dtype)
+        A_c_inv = torch.linalg.cholesky(vtv).inverse()
+        B_c = torch.linalg.cholesky(vtv + eye)
+        C = A_c_inv.t() @ (B_c - eye) @ A_c_inv
+        L_c = (C.inverse() + vtv).inverse()
+        return reg_lambda[:, None] * L_c * reg_lambda[None, :]
+
+    @staticmethod
+    def sampler(frst_eigvecs: Tensor, scnd_eigvecs: Tensor, reg_inv_correction: Tensor,
+                pre_sample: Tensor) -> Tensor:
+        """curvatures.py:582-612."""
+        X = torch.randn(frst_eigvecs.shape[0] * scnd_eigvecs.shape[0], device=frst_eigvecs.device,
+                        dtype=frst_eigvecs.dtype)
+        Y_l = reg_inv_correction * X
+        unvec_Y_l = Y_l.reshape((scnd_eigvecs.shape[0], frst_eigvecs.shape[0]))
+        Xq = scnd_eigvecs.t() @ unvec_Y_l @ frst_eigvecs
+        Qx = pre_sample @ Xq.t().contiguous().view(-1)
+        unvec_Qx = Qx.reshape((scnd_eigvecs.shape[1], frst_eigvecs.shape[1]))
+        X_p_s = scnd_eigvecs @ unvec_Qx @ frst_eigvecs.t()
+        Y_r = reg_inv_correction ** 2 * X_p_s.t().contiguous().view(-1)
+        return Y_l - Y_r
+
+    @staticmethod
+    def _dim_reduction(frst_eigvecs: Tensor, scnd_eigvecs: Tensor, lambda_vec: Tensor, rank: int):
+        """curvatures.py:614-660: the rows (a) and columns (g) of the top-`rank` |lambda|
+        entries of the (nA x nG) lambda grid, each set unique and ascending, and the
+        lambda sub-grid they span (row-major)."""
+        if rank >= lambda_vec.shape[0]:
+            return frst_eigvecs, scnd_eigvecs, lambda_vec
+        m = scnd_eigvecs.shape[1]
+        top = torch.argsort(-torch.abs(lambda_vec))[:rank]
+        left = torch.unique(top // m)
+        right = torch.unique(top % m)
+        lr_lambda = lambda_vec.view(-1, m)[left][:, right].reshape(-1)
+        return frst_eigvecs[:, left], scnd_eigvecs[:, right], lr_lambda
+
+    @staticmethod
+    def _diagonal_accumulator(xxt_eigvecs: Tensor, ggt_eigvecs: Tensor, lambda_vec: Tensor):
+        """curvatures.py:662-682: diag[i*m + j] = sum_{p,q} U_A[i,p]^2 U_G[j,q]^2
+        Lambda[p,q]; the reference's row loop over kron(U_A[i], U_G)^2 as one GEMM chain."""
+        lam = lambda_vec.view(xxt_eigvecs.shape[1], ggt_eigvecs.shape[1])
+        return ((xxt_eigvecs ** 2) @ lam @ (ggt_eigvecs ** 2).t()).reshape(-1)

@@ -210,6 +210,60 @@ def efb_sample(V_A, V_G, inv_lambdas, z, dtype=np.float64) -> np.ndarray:
     return (V_A @ (z * il.T) @ V_G.T).T
 
 
+# ------------------------------------------------------------------------------ INF
+# Literal restatements (loops and the materialised kron) of models/curvatures.py:476-682,
+# for small cases; the reference's INF cannot run on torch >= 2.0 either (it calls
+# get_eigenvectors), so these are pinned by the reference's lines only.
+def inf_dim_reduction(U_A, U_G, lambda_vec, rank):
+    """curvatures.py:614-660 (1-based index arithmetic kept)."""
+    lambda_vec = np.asarray(lambda_vec)
+    if rank >= lambda_vec.shape[0]:
+        return U_A, U_G, lambda_vec
+    m = U_G.shape[1]
+    idx_top = np.argsort(-np.abs(lambda_vec), kind="stable")[:rank] + 1
+    left = sorted({int((i - 1.) / m + 1.) for i in idx_top})
+    right = sorted({int(i - m * (int((i - 1.) / m + 1.) - 1)) for i in idx_top})
+    lm = [m * (i - 1) + j for i in left for j in right]
+    return (U_A[:, [i - 1 for i in left]], U_G[:, [j - 1 for j in right]],
+            lambda_vec[[k - 1 for k in lm]])
+
+
+def inf_diagonal_accumulator(U_A, U_G, lambda_vec, dtype=np.float64):
+    """curvatures.py:662-682: row loop over kron(U_A[i], U_G)^2 @ lambda."""
+    U_A, U_G, lambda_vec = (np.asarray(t, dtype=dtype) for t in (U_A, U_G, lambda_vec))
+    n, m = U_A.shape[0], U_G.shape[0]
+    out = np.zeros(n * m, dtype=dtype)
+    for i in range(n):
+        out[i * m:(i + 1) * m] = (kron(U_A[i:i + 1, :], U_G) ** 2) @ lambda_vec
+    return out
+
+
+def inf_pre_sampler(U_A, U_G, reg_lambda, reg_inv_correction, dtype=np.float64):
+    """curvatures.py:548-580 with the kron materialised."""
+    U_A, U_G, rl, ric = (np.asarray(t, dtype=dtype) for t in (U_A, U_G, reg_lambda, reg_inv_correction))
+    S = np.diag(rl)
+    V_s = ric.reshape(-1, 1) * kron(U_A, U_G) @ S
+    vtv = V_s.T @ V_s
+    vtv = (vtv + vtv.T) / 2.
+    eye = np.eye(S.shape[0])
+    A_c_inv = np.linalg.inv(np.linalg.cholesky(vtv))
+    B_c = np.linalg.cholesky(vtv + eye)
+    C = A_c_inv.T @ (B_c - eye) @ A_c_inv
+    L_c = np.linalg.inv(np.linalg.inv(C) + vtv)
+    return S @ L_c @ S
+
+
+def inf_sampler(U_A, U_G, reg_inv_correction, pre_sample, X, dtype=np.float64):
+    """curvatures.py:582-612, X the caller's N(0, 1) draw of length nA*nG."""
+    U_A, U_G, ric, P, X = (np.asarray(t, dtype=dtype) for t in (U_A, U_G, reg_inv_correction,
+                                                                pre_sample, X))
+    Y_l = ric * X
+    Xq = U_G.T @ Y_l.reshape(U_G.shape[0], U_A.shape[0]) @ U_A
+    Qx = P @ Xq.T.reshape(-1)
+    X_p_s = U_G @ Qx.reshape(U_G.shape[1], U_A.shape[1]) @ U_A.T
+    return Y_l - ric ** 2 * X_p_s.T.reshape(-1)
+
+
 # -------------------------------------------------------------- predictive variance
 def kron_quadform(J: np.ndarray, K1: np.ndarray, K2: np.ndarray, dtype=np.float64) -> np.ndarray:
     """v_b = J_b kron(K1, K2) J_b^T for each row b of J, without forming the kron.
