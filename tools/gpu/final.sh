@@ -1,2 +1,9 @@
+# Round-end check on the committed tree: GPU suite, smoke, default bench line.
 set -o pipefail
-timeout -k 10 900 bash profiles/collect.sh r01 && timeout -k 10 600 python bench.py > gpurun_out/bench_full.log 2>&1; tail -1 gpurun_out/bench_full.log
+mkdir -p gpurun_out
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/gpu_tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
+timeout -k 10 600 python bench.py > gpurun_out/bench_mlp.log 2>&1 || exit $?
+tail -1 gpurun_out/bench_mlp.log | cut -c1-300
