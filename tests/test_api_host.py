@@ -233,3 +233,44 @@ def test_variance_helpers():
     # classification_ll_block.py:119-121: every argmax column set in EVERY row
     assert torch.equal(go, torch.tensor([[1., 1., 0.], [1., 1., 0.]]))
     assert abs(entropy_bits(1.0) - 0.5 * np.log2(2 * np.e * np.pi)) < 1e-12
+
+
+def test_inf_host_algebra_matches_literal_oracle():
+    """INF's tensor restatements (curvatures.py:614-682: index arithmetic, the per-row
+    kron loop; :548-580 the pre-sample) against the literal loop/kron oracle.  These
+    are torch algebra on whatever device the tensors live; here CPU, no kernel call."""
+    import numpy as np
+    import torch
+    from bnn_kfac_amd.curvatures import INF
+    from oracle import kfac_oracle as O
+    rng = np.random.default_rng(3)
+    U_A = np.linalg.qr(rng.standard_normal((9, 9)))[0]
+    U_G = np.linalg.qr(rng.standard_normal((4, 4)))[0]
+    lam = rng.random(36) + 0.1
+    for rank in (1, 5, 17, 36, 100):
+        a, b, lr = INF._dim_reduction(*(torch.from_numpy(x) for x in (U_A, U_G, lam)), rank)
+        wa, wb, wl = O.inf_dim_reduction(U_A, U_G, lam, rank)
+        np.testing.assert_array_equal(a.numpy(), wa)
+        np.testing.assert_array_equal(b.numpy(), wb)
+        np.testing.assert_array_equal(lr.numpy(), wl)
+        d = INF._diagonal_accumulator(a, b, lr).numpy()
+        np.testing.assert_allclose(d, O.inf_diagonal_accumulator(wa, wb, wl), rtol=1e-12)
+        sig = np.sqrt(200 * np.asarray(wl))
+        c = 1.0 / np.sqrt(200 * rng.random(36) + 0.04)
+        P = INF.pre_sampler(a, b, torch.from_numpy(sig), torch.from_numpy(c)).numpy()
+        np.testing.assert_allclose(P, O.inf_pre_sampler(wa, wb, sig, c), rtol=1e-8, atol=1e-12)
+
+
+def test_sample_has_no_cpu_fallback():
+    """KFAC.sample / sample_and_replace go through kfac_sample only: host tensors raise."""
+    import pytest
+    import torch
+    from bnn_kfac_amd import _native as N
+    from bnn_kfac_amd.curvatures import KFAC
+    net = torch.nn.Sequential(torch.nn.Linear(6, 3))
+    kfac = KFAC(net)
+    kfac.inv_state = {net[0]: (torch.eye(7), torch.eye(3))}
+    with pytest.raises(N.NativeError):
+        kfac.sample(net[0])
+    with pytest.raises(N.NativeError):
+        kfac.sample_and_replace()
