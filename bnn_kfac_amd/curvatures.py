@@ -793,6 +793,7 @@ class KFAC(Curvature):
         assert self.inv_state, "Inverse state dict is empty. Did you call 'invert' prior to this?"
         first, second = self.inv_state[layer]
         z = torch.randn(first.size(0), second.size(0), device=first.device, dtype=first.dtype)
+        first, second = first.contiguous(), second.contiguous()
         out = torch.empty(second.size(0), first.size(0), device=first.device, dtype=first.dtype)
         N.sample([N.sample_job(first, second, z, out, first.size(0))], first.device, accumulate=False)
         return out
@@ -816,7 +817,10 @@ class KFAC(Curvature):
             first, second = inv_state[layer]
             nA, nG = first.size(0), second.size(0)
             z = torch.randn(nA, nG, device=first.device, dtype=first.dtype)
-            draws.append(z)
+            # row-major factors (a column-major one, e.g. from torch.linalg.cholesky,
+            # is copied; the copy is kept with the draws)
+            first, second = first.contiguous(), second.contiguous()
+            draws.extend((z, first, second))
             weight, bias = layer.weight.data, layer.bias.data if layer.bias is not None else None
             wcols = nA - 1 if bias is not None else nA
             if not weight.is_contiguous() or weight.numel() != nG * wcols:
@@ -887,6 +891,7 @@ class EFB(Curvature):
         lambdas = self.inv_state[layer]
         z = torch.randn(first.size(0), second.size(0), device=first.device, dtype=first.dtype)
         z *= lambdas.t()
+        first, second = first.contiguous(), second.contiguous()
         out = torch.empty(second.size(0), first.size(0), device=first.device, dtype=first.dtype)
         N.sample([N.sample_job(first, second, z, out, first.size(0), dense=True)], first.device,
                  accumulate=False)
