@@ -127,8 +127,12 @@ class Curvature(ABC):
 
     def save(self, filename):
         names = self._names()
-        torch.save({'state': {names[k]: list(v) for k, v in self.state.items()},
-                    'inv_state': {names[k]: list(v) for k, v in self.inv_state.items()},
+        # per-layer values are [A, G] / (L_A, L_G) (KFAC), tuples (INF) or one tensor (EFB)
+        def keep(v):
+            return list(v) if isinstance(v, (list, tuple)) else v
+
+        torch.save({'state': {names[k]: keep(v) for k, v in self.state.items()},
+                    'inv_state': {names[k]: keep(v) for k, v in self.inv_state.items()},
                     'model': self.model.state_dict()}, filename)
         print('Writting %s complete!\n' % filename)
 
@@ -136,8 +140,10 @@ class Curvature(ABC):
         blob = torch.load(filename, weights_only=True)
         modules = dict(self.model.named_modules())
         self.model.load_state_dict(blob['model'])
-        self.state = {modules[k]: list(v) for k, v in blob['state'].items()}
-        self.inv_state = {modules[k]: tuple(v) for k, v in blob['inv_state'].items()}
+        self.state = {modules[k]: list(v) if isinstance(v, list) else v
+                      for k, v in blob['state'].items()}
+        self.inv_state = {modules[k]: tuple(v) if isinstance(v, list) else v
+                          for k, v in blob['inv_state'].items()}
         print('Loading %s complete!\n' % filename)
 
 

@@ -117,3 +117,17 @@ def test_inf_vs_literal_oracle(hip_device, rank):
         X = torch.randn(a.shape[0] * b.shape[0], device=hip_device).cpu().numpy()
         want = O.inf_sampler(a, b, c, P, X).reshape(a.shape[0], b.shape[0]).T
         np.testing.assert_allclose(s, want, rtol=1e-4, atol=1e-4 * np.abs(want).max())
+
+
+def test_efb_save_load_roundtrip(hip_device, tmp_path):
+    """Curvature.save/load (curvatures.py:132-144) with EFB's per-layer tensors."""
+    from bnn_kfac_amd.curvatures import EFB
+    net, factors, efb, _ = _setup(hip_device)
+    efb.invert(0.04, 200.0)
+    fn = str(tmp_path / "efb.pt")
+    efb.save(fn)
+    other = EFB(net, factors)
+    other.load(fn)
+    for m in (net[0], net[3]):
+        assert torch.equal(other.state[m], efb.state[m])
+        assert torch.equal(other.inv_state[m], efb.inv_state[m])
