@@ -1,6 +1,6 @@
 """Turn a profiles/collect.sh run (gpurun_out/prof_<tag>/) into the committed summaries.
 
-    python profiles/summarize.py r01
+    python profiles/summarize.py r01          (r01_wide etc.: other configs, same recipe)
 
 writes
   profiles/<tag>/kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
@@ -57,8 +57,11 @@ def main(tag):
                "rocprof_trace": stats.get("kfac_factor_tiles"),
                "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->bytes, "
                        "mean over the bench's launches (15 updates per pass, last batch short)"}
-        with open(os.path.join(ROOT, "profiles", "factor_tiles_pmc.json"), "w") as f:
+        with open(os.path.join(dst, "factor_tiles_hbm.json"), "w") as f:
             json.dump(out, f, indent=1)
+        if "_" not in tag:  # the headline (MLP) profile: the file bench.py reads
+            with open(os.path.join(ROOT, "profiles", "factor_tiles_pmc.json"), "w") as f:
+                json.dump(out, f, indent=1)
         print(json.dumps(out, indent=1))
 
 
