@@ -4,23 +4,38 @@
     python bench.py [--gpus N --steps K --warmup W] [--config mlp|lenet|wide]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+`--gpus N > 1` without a launcher's WORLD_SIZE: this process spawns the N rank
+processes itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / a free
+MASTER_PORT in each child's env) and never touches the GPU (spawn_ranks).
+
 One STEP = one KFAC data pass over `--images` synthetic images per rank in batches
 of `--batch` (one KFAC.update per batch, activations/gradients already resident in
 HBM, records injected exactly as the reference's hooks leave them) + the packed
-RCCL all-reduce (N > 1) + KFAC.invert(0.04, 200) (models/curvatures.py:325-398;
-damping of classification_ll_block.py:72-73,106).  Weak scaling: every rank
-processes the same per-rank workload; `value` = all ranks' images / wall time.
+RCCL all-reduce of the factors' lower triangles (N > 1) + KFAC.invert(0.04, 200)
+(models/curvatures.py:325-398; damping of classification_ll_block.py:72-73,106),
+every inversion's pivot verdict read back inside the timed region.  Weak scaling:
+every rank processes the same per-rank workload; `value` = all ranks' images / the
+slowest rank's wall time.
+
+Workloads (BASELINE.json configs): N = 1 runs C2 (MLP, batch 4096, 60,000 images);
+N > 1 runs C4's per-rank shard (MLP, 8,192 rows per rank of each global batch
+N x 8,192 -- 65,536 at N = 8 -- over 65,536 images per rank); `--config lenet` is
+C3 (batch 1024), `--config wide` is C5.
 
 Also reported (same JSON line): the roofline of the dominant kernel
 (kfac_factor_tiles, fp32 MFMA; HIP-event durations measured live on its stream),
-the pass/invert split, an end-to-end variant (forward + Categorical label sample
-+ CE backward + update + invert), and the CPU baseline: the reference's op
-sequence (oracle/cpu_ref_torch.py, torch CPU fp32) on a bounded sample of the
-same workload, on this host's cores.
+the pass/all-reduce/invert split, the serial rate (one pass, then invert on the
+caller's stream, then the verdict read: the latency a caller who does not pipeline
+passes sees), an end-to-end variant (forward + Categorical label sample + CE
+backward + update + invert), and the CPU baseline: the reference's op sequence
+(oracle/cpu_ref_torch.py, torch CPU fp32) on a bounded sample of the same
+workload, on this host's cores (and on 1 thread).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -62,6 +77,12 @@ CONFIGS = {
               Layer("linear", 400, 120), Layer("linear", 120, 84), Layer("linear", 84, 10)],
 }
 NAMES = {"mlp": "MLP 784-128-10", "wide": "Wide MLP 784-4096-4096-10", "lenet": "LeNet-5"}
+# (batch per rank, images per rank): C2 at N = 1, C4's shard at N > 1, C3, C5
+SHAPES = {("mlp", 1): (4096, 60000), ("mlp", 2): (8192, 65536),
+          ("lenet", 1): (1024, 60000), ("lenet", 2): (1024, 60000),
+          ("wide", 1): (4096, 16384), ("wide", 2): (4096, 16384)}
+BASELINE_CONFIG = {("mlp", 1): "C2", ("mlp", 2): "C4", ("lenet", 1): "C3", ("lenet", 2): "C3",
+                   ("wide", 1): "C5", ("wide", 2): "C5"}
 
 
 def flops_per_image(layers):
@@ -101,18 +122,30 @@ def synthetic_records(layers, images, device, seed):
              torch.randn(images, *l.out_shape, device=device, generator=g)) for l in layers]
 
 
-def cpu_baseline(layers, images, batch, budget_s=12.0):
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(layers, images, batch, budget_s=12.0, threads=None):
     """The reference's CPU op sequence (oracle/cpu_ref_torch.py) on the same workload,
-    bounded to ~budget_s seconds of whole passes; returns (images/s, cores, sample)."""
+    bounded to ~budget_s seconds of batches (whole passes when they fit; else the
+    batches done so far plus one inversion); returns (images/s, threads, sample)."""
     from oracle import cpu_ref_torch as C
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    if threads is None:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     torch.set_num_threads(threads)
     rng = np.random.default_rng(0)
     recs = [(torch.from_numpy(rng.random((images, *l.in_shape), dtype=np.float32)),
              torch.from_numpy(rng.standard_normal((images, *l.out_shape), dtype=np.float32)))
             for l in layers]
-    done, t0 = 0, time.perf_counter()
-    passes = 0
+    done, passes, t0 = 0, 0, time.perf_counter()
     while True:
         state = {}
         for i in range(0, images, batch):
@@ -121,41 +154,120 @@ def cpu_baseline(layers, images, batch, budget_s=12.0):
                     C.linear_update(state, li, a[i:i + batch], gr[i:i + batch], True)
                 else:
                     C.conv_update(state, li, a[i:i + batch], gr[i:i + batch], l.k, l.pad, l.stride, True)
+            done += min(batch, images - i)
+            if time.perf_counter() - t0 >= budget_s and i + batch < images:
+                break  # a partial pass: its batches plus one inversion below
         C.invert(state, *DAMPING)
-        done += images
         passes += 1
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
-    return done / dt, threads, (f"{passes} full pass(es) of {images} synthetic images, batch {batch}, "
-                                f"update+invert, torch {torch.__version__} CPU fp32, {threads} threads")
+    return done / dt, threads, (f"{done} synthetic images in {passes} pass(es) of up to {images}, "
+                                f"batch {batch}, update+invert per pass, torch {torch.__version__} CPU "
+                                f"fp32, {threads} thread(s)")
 
 
-def load_traffic():
-    path = os.path.join(ROOT, "profiles", "factor_tiles_pmc.json")
+def load_traffic(config):
+    name = "factor_tiles_pmc.json" if config == "mlp" else f"factor_tiles_pmc_{config}.json"
+    path = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(path):
         return None
     with open(path) as f:
         return json.load(f).get("hbm_bytes_per_launch")
 
 
-def main():
+# ------------------------------------------------------------------ launcher
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv, cmd=None, check_devices=True, poll_s=0.2):
+    """Run `n` rank processes of this script (or of `cmd`) on one node and return the
+    worst exit code.  Each child gets RANK = LOCAL_RANK = r, WORLD_SIZE =
+    LOCAL_WORLD_SIZE = n, MASTER_ADDR = 127.0.0.1 and one free MASTER_PORT; it sets
+    its own device and joins the process group.  The parent makes no HIP call
+    (torch.cuda.device_count() does not initialise the runtime on this image), so a
+    rank's GPU work never shares a process with another's.  When one rank fails,
+    the others are terminated (their exact PIDs)."""
+    if check_devices:
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py --gpus {n}: only {have} GPU(s) visible on this node; need {n} "
+                  f"(one rank per GPU)", file=sys.stderr, flush=True)
+            return 2
+    port = _free_port()
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)] + list(argv)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen(cmd, env=env))
+    codes = [None] * n
+    first_bad = 0
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None:
+                codes[i] = p.poll()
+                if codes[i] not in (None, 0) and not first_bad:
+                    first_bad = codes[i] if codes[i] > 0 else 1
+        if first_bad:
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    try:
+                        codes[i] = p.wait(timeout=20)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        codes[i] = p.wait()
+            break
+        time.sleep(poll_s)
+    return first_bad
+
+
+# ------------------------------------------------------------------ one rank
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="mlp", choices=sorted(CONFIGS))
-    ap.add_argument("--batch", type=int, default=4096, help="per-rank batch")
-    ap.add_argument("--images", type=int, default=60000, help="images per rank per pass")
+    ap.add_argument("--batch", type=int, default=None, help="per-rank batch (default: the config's)")
+    ap.add_argument("--images", type=int, default=None, help="images per rank per pass")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-serial", action="store_true")
     ap.add_argument("--partition", type=int, default=0,
                     help="CUs reserved for the overlapped inversion (KFAC.partition_cus; 0 = none)")
-    args = ap.parse_args()
+    argv = sys.argv[1:] if argv is None else argv
+    args = ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            return spawn_ranks(args.gpus, argv)
+        world = 1
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus and not (args.gpus == 1 and world > 1):
+            print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks",
+                  file=sys.stderr, flush=True)
+            return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.device_count() <= local:
+        print(f"bench.py rank {rank}: LOCAL_RANK {local} but only {torch.cuda.device_count()} GPU(s) "
+              f"visible", file=sys.stderr, flush=True)
+        return 2
+    shape_key = (args.config, 1 if world == 1 else 2)
+    batch, images = SHAPES[shape_key]
+    batch = args.batch or batch
+    images = args.images or images
+
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
@@ -173,15 +285,32 @@ def main():
     layers = [m for m in net.modules() if isinstance(m, (torch.nn.Linear, torch.nn.Conv2d))]
     kfac = DistributedKFAC(net) if world > 1 else KFAC(net)
     kfac.partition_cus = args.partition
-    recs = synthetic_records(specs, args.images, device, seed=1234 + rank)
-    starts = list(range(0, args.images, args.batch))
+    recs = synthetic_records(specs, images, device, seed=1234 + rank)
+    starts = list(range(0, images, batch))
+    comm = {"ms": 0.0, "n": 0, "timing": False}
+
+    if world > 1:
+        # the instrumented repetition times the collective with events on the
+        # caller's stream (the collective's own stream is joined into it both ways)
+        _allreduce = kfac.allreduce
+
+        def timed_allreduce():
+            if not comm["timing"] or not kfac._pending:
+                return _allreduce()
+            kfac.flush()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            _allreduce()
+            e1.record()
+            comm.setdefault("events", []).append((e0, e1))
+        kfac.allreduce = timed_allreduce
 
     def one_pass():
         kfac.reset()
         for i in starts:
             for layer, (a, g) in zip(layers, recs):
-                kfac.record[layer] = [a[i:i + args.batch], g[i:i + args.batch]]
-            kfac.update(batch_size=min(args.batch, args.images - i))
+                kfac.record[layer] = [a[i:i + batch], g[i:i + batch]]
+            kfac.update(batch_size=min(batch, images - i))
         kfac.invert(*DAMPING)
 
     def sync():
@@ -189,65 +318,98 @@ def main():
         if world > 1:
             dist.barrier()
 
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t)
+
     for _ in range(args.warmup):
         one_pass()
+    kfac.inv_state  # settle the warmup's verdicts
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_pass()
+    # inside the timed region: join the inversion worker and read every pending
+    # pivot verdict (a singular factor raises here, as the reference's would)
+    kfac.inv_state
     sync()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+
     # Kernel durations: the same K steps again with the library's HIP-event timing
     # on (events recorded around each launch, on its stream).  Kept out of the timed
     # region above because the event packets add ~10 us per launch boundary.
     N.profile_reset()
     N.profile_enable(True)
+    comm["timing"] = True
     for _ in range(args.steps):
         one_pass()
+    kfac.inv_state
     sync()
+    comm["timing"] = False
     N.profile_enable(False)
     tiles_ms, tiles_n = N.profile_read(N.PROF_FACTOR_TILES)
     red_ms, red_n = N.profile_read(N.PROF_FACTOR_REDUCE)
     inv_ms, inv_n = N.profile_read(N.PROF_INVERT)
     N.profile_reset()
+    allreduce_ms = None
+    if world > 1:
+        allreduce_ms = max_over_ranks(sum(a.elapsed_time(b) for a, b in comm.pop("events", []))
+                                      / args.steps)
 
-    images_total = world * args.images * args.steps
+    images_total = world * images * args.steps
     value = images_total / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
 
-    # roofline of the dominant kernel: algorithmic flops of one launch (= one
-    # update of one batch) / its measured duration, averaged over the timed region
+    # roofline of the dominant kernel: algorithmic flops of one launch (= the queued
+    # updates it covers) / its measured duration, averaged over the timed region
     fpi = flops_per_image(specs)
-    flops_timed = fpi * args.images * args.steps
+    flops_timed = fpi * images * args.steps
     achieved = flops_timed / (tiles_ms * 1e-3) / 1e12 if tiles_ms > 0 else None
-    traffic = load_traffic() if args.config == "mlp" else None  # PMC summary is of the MLP run
     roofline = {"bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": (achieved / MFMA_F32_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
+                "frac": (achieved / MFMA_F32_PEAK_TFLOPS) if achieved else None,
+                "traffic": load_traffic(args.config),
                 "kernel": "kfac_factor_tiles", "launches": tiles_n,
                 "avg_launch_us": 1e3 * tiles_ms / max(tiles_n, 1),
                 # a launch covers every queued update of the pass (multi-batch jobs):
                 # per-launch figures are the step's algorithmic totals / its launches
-                "flops_per_launch": fpi * args.images * args.steps / max(tiles_n, 1),
-                "algorithmic_bytes_per_launch": bytes_per_image(specs) * args.images * args.steps
+                "flops_per_launch": fpi * images * args.steps / max(tiles_n, 1),
+                "algorithmic_bytes_per_launch": bytes_per_image(specs) * images * args.steps
                                                 / max(tiles_n, 1)}
     breakdown = {"factor_tiles_ms_per_step": tiles_ms / args.steps,
                  "factor_reduce_ms_per_step": red_ms / args.steps,
                  "invert_ms_per_step": inv_ms / args.steps,
+                 "allreduce_ms_per_step": allreduce_ms,
                  "updates_per_step": len(starts)}
+
+    serial = None
+    if not args.no_serial:
+        # the caller who runs a pass, inverts on its own stream and reads the result
+        # before the next pass (classification_ll_block.py:93-106): no overlap
+        kfac.overlap_invert = False
+        one_pass()
+        kfac.inv_state
+        sync()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            one_pass()
+            kfac.inv_state
+            torch.cuda.synchronize(device)
+        sync()
+        serial = world * images * args.steps / max_over_ranks(time.perf_counter() - t1)
+        kfac.overlap_invert = True
 
     e2e = None
     if not args.no_e2e and world == 1:
-        x = torch.rand(args.images, *specs[0].in_shape, device=device)
+        x = torch.rand(images, *specs[0].in_shape, device=device)
         crit = torch.nn.CrossEntropyLoss()
 
         def e2e_pass():
             kfac.reset()
             for i in starts:
-                logits = net(x[i:i + args.batch])
+                logits = net(x[i:i + batch])
                 labels = torch.distributions.Categorical(logits=logits).sample()
                 loss = crit(logits, labels)
                 net.zero_grad()
@@ -255,34 +417,46 @@ def main():
                 kfac.update(batch_size=logits.shape[0])
             kfac.invert(*DAMPING)
         e2e_pass()
+        kfac.inv_state
         sync()
         t1 = time.perf_counter()
         reps = max(1, args.steps // 2)
         for _ in range(reps):
             e2e_pass()
+        kfac.inv_state
         sync()
-        e2e = args.images * reps / (time.perf_counter() - t1)
+        e2e = images * reps / (time.perf_counter() - t1)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        v, cores, sample = cpu_baseline(specs, args.images, args.batch)
-        cpu = {"value": v, "unit": "images/s", "cores": cores, "kind": "port", "sample": sample}
+        v, cores, sample = cpu_baseline(specs, images, batch)
+        v1, _, sample1 = cpu_baseline(specs, images, batch, budget_s=6.0, threads=1)
+        cpu = {"value": v, "unit": "images/s", "cores": cores, "kind": "port", "sample": sample,
+               "value_1_thread": v1, "sample_1_thread": sample1, "cpu_model": cpu_model(),
+               "logical_cpus_visible": os.cpu_count()}
 
     if rank == 0:
+        cfg = BASELINE_CONFIG[shape_key]
         out = {"metric": METRIC, "value": value, "unit": "images/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
                "data": "synthetic (resident U[0,1) activations, N(0,1) output-gradient records)",
-               "config": {"workload": f"{NAMES[args.config]} KFAC factor pass over {args.images} "
-                                      f"images/rank (batch {args.batch}/rank) + invert{DAMPING}",
-                          "global_batch": args.batch * world, "images_per_rank": args.images,
-                          "parallelism": f"dp{world}", "inversion_cus": args.partition or "shared"},
+               "config": {"workload": f"{cfg}: {NAMES[args.config]} KFAC factor pass over {images} "
+                                      f"images/rank (batch {batch}/rank, global batch {batch * world}) "
+                                      f"+ invert{DAMPING}",
+                          "baseline_config": cfg, "global_batch": batch * world,
+                          "images_per_rank": images, "parallelism": f"dp{world}",
+                          "inversion": ("sharded" if getattr(kfac, "_sharded_last", False)
+                                        else "replicated"),
+                          "inversion_cus": args.partition or "shared"},
                "roofline": roofline, "cpu_baseline": cpu, "breakdown": breakdown,
-               "e2e_images_per_s": e2e}
+               "allreduce_ms_per_step": allreduce_ms,
+               "serial_images_per_s": serial, "e2e_images_per_s": e2e}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -21,6 +21,7 @@ LIB_PATH = os.environ.get("BNN_KFAC_AMD_LIB", os.path.join(_HERE, "libkfac_hip.s
 KFAC_OK, KFAC_EINVAL, KFAC_ELAUNCH, KFAC_EWORKSPACE = 0, -1, -2, -3
 ROWMAJOR, CHANNEL, PATCH = 0, 1, 2
 OUT_INV_CHOL, OUT_INVERSE = 0, 1
+TRI_SYMMETRIC, TRI_LOWER = 0, 1
 PROF_FACTOR_TILES, PROF_FACTOR_REDUCE, PROF_INVERT, PROF_QUAD_TILES = 0, 1, 2, 3
 
 c_i32, c_i64, c_f32, c_f64, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_void_p
@@ -62,6 +63,10 @@ class SampleJob(ctypes.Structure):
                 ("wcols", c_i32), ("dense", c_i32)]
 
 
+class TriJob(ctypes.Structure):
+    _fields_ = [("F", c_vp), ("ldF", c_i64), ("n", c_i32), ("reserved", c_i32), ("offset", c_i64)]
+
+
 # symbol -> (restype, argtypes); every symbol include/kfac_hip.h declares
 SIGNATURES = {
     "kfac_factor_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(FactorJob), ctypes.c_int]),
@@ -96,6 +101,8 @@ SIGNATURES = {
                                    ctypes.c_size_t, c_vp]),
     "kfac_invert_phase": (ctypes.c_int, [ctypes.POINTER(InvertJob), ctypes.c_int, c_vp, ctypes.c_size_t,
                                          c_vp, ctypes.c_int, c_vp]),
+    "kfac_tri_pack": (ctypes.c_int, [ctypes.POINTER(TriJob), ctypes.c_int, c_vp, c_vp]),
+    "kfac_tri_unpack": (ctypes.c_int, [ctypes.POINTER(TriJob), ctypes.c_int, c_vp, ctypes.c_int, c_vp]),
     "kfac_cu_count": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "kfac_set_cu_budget": (ctypes.c_int, [ctypes.c_int]),
     "kfac_stream_create_cu_mask": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
@@ -251,6 +258,32 @@ def invert_phase(arr, ws: torch.Tensor, info: torch.Tensor, phase: int, stream: 
     """kfac_invert_phase (ctypes releases the GIL for the call: safe from a worker thread)."""
     check(lib().kfac_invert_phase(arr, len(arr), ws.data_ptr(), ws.numel(), info.data_ptr(), phase, stream),
           "kfac_invert_phase")
+
+
+def tri_jobs(factors):
+    """[TriJob] of square row-major factors laid out back to back in a packed
+    lower-triangle buffer, and that buffer's length (elements)."""
+    jobs, off = [], 0
+    for F in factors:
+        n = F.shape[0]
+        if F.dim() != 2 or F.shape[1] != n or F.stride(1) != 1:
+            raise NativeError(f"tri pack: factor must be square with unit column stride, got "
+                              f"{tuple(F.shape)} / {F.stride()}")
+        jobs.append(TriJob(F.data_ptr(), F.stride(0), n, 0, off))
+        off += n * (n + 1) // 2
+    return jobs, off
+
+
+def tri_pack(jobs, packed: torch.Tensor) -> None:
+    """kfac_tri_pack on torch's current stream of packed's device."""
+    check(lib().kfac_tri_pack(as_array(TriJob, jobs), len(jobs), packed.data_ptr(),
+                              stream_handle(packed.device)), "kfac_tri_pack")
+
+
+def tri_unpack(jobs, packed: torch.Tensor, mode: int) -> None:
+    """kfac_tri_unpack (TRI_SYMMETRIC mirrors, TRI_LOWER zeroes the upper triangle)."""
+    check(lib().kfac_tri_unpack(as_array(TriJob, jobs), len(jobs), packed.data_ptr(), int(mode),
+                                stream_handle(packed.device)), "kfac_tri_unpack")
 
 
 def cu_count(device: torch.device) -> int:

@@ -164,9 +164,14 @@ class KFAC(Curvature):
                 if layer.__class__.__name__ in ['Linear', 'Conv2d']:
                     self.record[layer] = [None, None]
                     self.hooks.append(layer.register_forward_pre_hook(self._save_input))
-                    # full hook: same grad_output[0] as the reference's legacy
-                    # register_backward_hook for Linear/Conv2d (curvatures.py:315)
-                    self.hooks.append(layer.register_full_backward_hook(self._save_output))
+                    # the reference's legacy module backward hook (curvatures.py:315) is a
+                    # hook on the grad_fn of the layer's own last op (addmm / convolution):
+                    # registered here the same way, from a forward hook, without the
+                    # deprecated API.  An in-place activation after the layer
+                    # (nn.ReLU(inplace=True), torchvision style) leaves that node intact,
+                    # so grad_output[0] is dL/d(out) as in the reference; a full backward
+                    # hook wraps the output in a view that such an op breaks at backward.
+                    self.hooks.append(layer.register_forward_hook(self._hook_output))
                 elif layer.__class__.__name__ == 'MultiheadAttention':
                     raise NotImplementedError
         self._packed = None      # flat fp32 device buffer holding every factor
@@ -314,6 +319,14 @@ class KFAC(Curvature):
 
     def _save_output(self, module, grad_input, grad_output):
         self.record[module][1] = grad_output[0] * grad_output[0].size(0)
+
+    def _hook_output(self, module, input, output):
+        """Forward hook: the backward hook of this call goes on the output's grad_fn
+        (what torch's legacy register_backward_hook does; no grad_fn -> no record)."""
+        fn = output.grad_fn if isinstance(output, Tensor) else None
+        if fn is not None:
+            fn.register_hook(lambda grad_input, grad_output: self._save_output(module, grad_input,
+                                                                                grad_output))
 
     # ------------------------------------------------------------------ update
     def _layers(self):
@@ -814,7 +827,7 @@ class KFAC(Curvature):
         self.model.load_state_dict(self.model_state)
         # the draws stay referenced until the launch is queued (a freed z would be
         # handed to the next draw by the caching allocator)
-        jobs, draws, device = [], [], None
+        jobs, draws, copies, device = [], [], [], None
         for layer in self.model.modules():
             if layer.__class__.__name__ not in self.layer_types:
                 continue
@@ -829,13 +842,22 @@ class KFAC(Curvature):
             draws.extend((z, first, second))
             weight, bias = layer.weight.data, layer.bias.data if layer.bias is not None else None
             wcols = nA - 1 if bias is not None else nA
-            if not weight.is_contiguous() or weight.numel() != nG * wcols:
-                raise N.NativeError(f"sample_and_replace: {layer} weight is not a contiguous "
-                                    f"({nG} x {wcols}) block")
-            jobs.append(N.sample_job(first, second, z, weight.view(nG, wcols), wcols, bias))
+            if weight.numel() != nG * wcols:
+                raise N.NativeError(f"sample_and_replace: {layer} weight has {weight.numel()} "
+                                    f"elements, its factors give {nG} x {wcols}")
+            target = weight
+            if not weight.is_contiguous():
+                # e.g. a channels_last Conv2d weight: the launch adds into a contiguous
+                # copy, written back afterwards (the reference's _replace adds through
+                # .contiguous().view(...) as well, curvatures.py:80-82)
+                target = weight.contiguous()
+                copies.append((weight, target))
+            jobs.append(N.sample_job(first, second, z, target.view(nG, wcols), wcols, bias))
             device = first.device
         if jobs:
             N.sample(jobs, device, accumulate=True)
+        for weight, target in copies:
+            weight.copy_(target)
 
 
 class EFB(Curvature):

@@ -7,10 +7,20 @@ reference's state when every rank accumulates
 
     sum_b (1 / B_global) * X_b,rank^T X_b,rank
 
-locally (alpha = 1/B_global instead of 1/B_local) and the ranks' packed factor
-buffers are summed ONCE after the pass (torch.distributed all_reduce; with the
-"nccl" backend that is RCCL over xGMI).  Inversion is then replicated on every
-rank (small factors) — no second collective.
+locally (alpha = 1/B_global instead of 1/B_local) and the ranks' factors are
+summed ONCE after the pass: their lower triangles are packed back to back into one
+buffer (kfac_tri_pack: n(n+1)/2 floats per factor, half the n^2), all-reduced by
+torch.distributed (the "nccl" backend is RCCL over xGMI) and unpacked with the
+upper triangle mirrored (kfac_tri_unpack).
+
+Inversion (curvatures.py:367-398) is then either
+* replicated on every rank (small, latency-bound factors: the MLP's; no second
+  collective, and the inversion overlaps the next pass as in KFAC), or
+* sharded (some factor > 1536, the throughput-bound case -- the wide MLP's
+  4096^2 factors): factors are assigned to ranks greedily by n^3 (largest first,
+  to the least-loaded rank), each rank inverts its own, and ONE all-gather hands
+  every rank all L factors (packed lower triangles + the pivot verdicts), so a
+  rank inverts ~1/world of the work instead of all of it.
 """
 from __future__ import annotations
 
@@ -20,7 +30,23 @@ import torch
 import torch.distributed as dist
 from torch.nn import Module, Sequential
 
+from . import _native as N
 from .curvatures import KFAC
+
+SHARD_MIN_N = 1536  # largest factor above this: the inversion is throughput-bound
+
+
+def assign_owners(sizes, world):
+    """Rank of each factor (sizes = n per factor, in job order): largest n^3 first,
+    each to the least-loaded rank (ties: lower rank, earlier factor).  Every rank
+    computes the same assignment from the same sizes."""
+    load = [0.0] * world
+    owner = [0] * len(sizes)
+    for i in sorted(range(len(sizes)), key=lambda i: (-sizes[i], i)):
+        r = min(range(world), key=lambda r: (load[r], r))
+        owner[i] = r
+        load[r] += float(sizes[i]) ** 3
+    return owner
 
 
 class DistributedKFAC(KFAC):
@@ -29,18 +55,28 @@ class DistributedKFAC(KFAC):
     `update(batch_size, global_batch_size=None)`: the per-batch mean is taken over
     the GLOBAL batch (default: world_size x the local rows, i.e. equal shards).
     Local contributions accumulate into a private packed buffer; `allreduce()`
-    (called by `invert()` if needed) sums it over ranks into `state`.
+    (called by `invert()`, and by any read of `state`, if needed) sums it over
+    ranks into `state`.  Reading `state` is therefore a collective call while a
+    pass is pending: every rank must do it.
+
+    `shard_inversion`: "auto" (shard when world > 1 and some factor is larger than
+    1536), True or False.
     """
 
     def __init__(self, model: Union[Module, Sequential], layer_types: Union[List[str], str] = None,
-                 process_group=None):
+                 process_group=None, shard_inversion="auto"):
         super().__init__(model, layer_types)
         self.group = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
+        self.shard_inversion = shard_inversion
+        self.always_reduce = False  # run the collectives even at world 1 (tests)
         self._scale = 1.0          # local rows -> global rows for the current update
         self._local_state = {}     # rank-local accumulation (views of the packed buffer)
         self._pending = False
         self._global_buf, self._global_views = None, {}
+        self._tri = {}             # name -> staging buffer of the packed-triangle collectives
+        self._sharded_last = False
 
     def _alpha(self, op) -> float:
         return 1.0 / (float(op.rows) * self._scale) if op.rows else float("inf")
@@ -61,23 +97,40 @@ class DistributedKFAC(KFAC):
             self._state = reduced
         self._pending = True
 
+    def flush(self):
+        """KFAC.flush, then the pass's all-reduce if one is pending (so `state` holds
+        every rank's updates, like the single-device state)."""
+        super().flush()
+        if getattr(self, "_pending", False):
+            self.allreduce()
+
+    def _collective(self):
+        return self.world > 1 or self.always_reduce
+
+    def _buffer(self, name, numel, device):
+        buf = self._tri.get(name)
+        if buf is None or buf.numel() < numel or buf.device != device:
+            buf = self._tri[name] = torch.empty(numel, dtype=torch.float32, device=device)
+        return buf[:numel]
+
     def allreduce(self):
-        """Sum the rank-local factors over ranks and add them to `state` (one collective)."""
+        """Sum the rank-local factors over ranks and add them to `state`: ONE
+        collective over the packed lower triangles of every factor."""
         if not self._pending:
             return
-        self.flush()  # the rank-local factors are complete only after the deferred reduce
+        KFAC.flush(self)  # the rank-local factors are complete only after the deferred reduce
         local = self._local_state
+        if self._collective() and local:
+            factors = [F for pair in local.values() for F in pair]
+            jobs, total = N.tri_jobs(factors)
+            buf = self._buffer("reduce", total, factors[0].device)
+            N.tri_pack(jobs, buf)
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+            N.tri_unpack(jobs, buf, N.TRI_SYMMETRIC)
         packed = self._packed
         views_packed = packed is not None and all(
             local[layer][0].data_ptr() == self._packed_views[layer][0].data_ptr() for layer in local)
-        if self.world > 1:
-            if views_packed:
-                dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=self.group)
-            else:
-                for A, G in local.values():
-                    dist.all_reduce(A, group=self.group)
-                    dist.all_reduce(G, group=self.group)
-        if not self._state:
+        if not self._state and views_packed:
             # first pass: the reduced local buffer becomes the state (no copy); the next
             # local accumulation gets a fresh buffer
             self._state = {layer: list(v) for layer, v in local.items()}
@@ -94,9 +147,94 @@ class DistributedKFAC(KFAC):
         self._local_state = {}
         self._pending = False
 
+    def _shard_now(self, entries):
+        if not self._collective():
+            return False
+        if self.shard_inversion == "auto":
+            return self.world > 1 and max(F_.shape[0] for _, v in entries for F_ in v) > SHARD_MIN_N
+        return bool(self.shard_inversion)
+
     def invert(self, add=0., multiply=1.):
         self.allreduce()
-        return super().invert(add, multiply)
+        assert self.state, "State dict is empty. Did you call 'update' prior to this?"
+        entries = list(self.state.items())
+        self._sharded_last = self._shard_now(entries)
+        if not self._sharded_last:
+            return super().invert(add, multiply)
+        return self._invert_sharded(entries, add, multiply)
+
+    def _invert_sharded(self, entries, add, multiply):
+        """Each rank inverts the factors it owns (one grouped kfac_invert on the
+        caller's stream), then ONE all-gather gives every rank every L factor.  A
+        rank's segment of the gather: its jobs' pivot verdicts (as floats, exact for
+        any n < 2^24) in the first `slots` entries, then its L factors' packed lower
+        triangles.  The verdicts are read back like KFAC.invert's (deferred)."""
+        self._defer_verdict()
+        if self._inv_state:
+            Warning("State has already been inverted. Is this expected?")
+        damping = self._damping(add, multiply)
+        factors, params = [], []
+        for (layer, value), (n, s) in zip(entries, damping):
+            for F_ in value:
+                N.require_device(F_, "state", layer)
+                factors.append(F_)
+                params.append((s ** 0.5, n ** 0.5))
+        device = factors[0].device
+        world, me = max(self.world, 1), self.rank
+        owner = assign_owners([F_.shape[0] for F_ in factors], world)
+        outs = [torch.empty_like(F_, memory_format=torch.contiguous_format) for F_ in factors]
+        slots = max(sum(1 for o in owner if o == r) for r in range(world))
+        tri = [F_.shape[0] * (F_.shape[0] + 1) // 2 for F_ in factors]
+        seg = slots + max(sum(t for t, o in zip(tri, owner) if o == r) for r in range(world))
+        # where job i sits in the gathered buffer: (verdict index, triangle offset)
+        where, fill = [], [0] * world
+        toff = [slots] * world
+        for i, r in enumerate(owner):
+            where.append((r * seg + fill[r], r * seg + toff[r]))
+            fill[r] += 1
+            toff[r] += tri[i]
+        mine = [i for i in range(len(factors)) if owner[i] == me]
+        send = self._buffer("gather_send", seg, device)
+        recv = self._buffer("gather_recv", world * seg, device)
+        if mine:
+            jobs = [N.invert_job(factors[i], outs[i], *params[i]) for i in mine]
+            info = N.invert(jobs, device)
+            send[:len(mine)].copy_(info)
+            N.tri_pack([N.TriJob(outs[i].data_ptr(), outs[i].stride(0), outs[i].shape[0], 0,
+                                 where[i][1] - me * seg) for i in mine], send)
+        if self.world > 1:
+            self._all_gather(recv, send)
+        else:
+            recv.copy_(send)
+        others = [N.TriJob(outs[i].data_ptr(), outs[i].stride(0), outs[i].shape[0], 0, where[i][1])
+                  for i in range(len(factors)) if owner[i] != me]
+        if others:
+            N.tri_unpack(others, recv, N.TRI_LOWER)
+        idx = torch.tensor([w[0] for w in where], dtype=torch.int64).to(device, non_blocking=True)
+        info_all = recv.index_select(0, idx).to(torch.int32)
+        done, host = self._readback(info_all)
+        layers = [layer for layer, _ in entries]
+        for k, layer in enumerate(layers):
+            self._inv_state[layer] = (outs[2 * k], outs[2 * k + 1])
+        self._inv_pending = (done, host, layers, self._inv_state, outs, False, False, None)
+
+    def _readback(self, info):
+        """(event, pinned host copy) of a device verdict vector, copied without a
+        host wait on the caller's stream (settled at the next inv_state read)."""
+        pool = self._info_pool
+        while pool and pool[-1].numel() != info.numel():
+            pool.pop()
+        host = pool.pop() if pool else torch.empty(info.numel(), dtype=torch.int32, pin_memory=True)
+        host.copy_(info, non_blocking=True)
+        done = torch.cuda.Event()
+        done.record()
+        return done, host
+
+    def _all_gather(self, recv, send):
+        if dist.get_backend(self.group) == "gloo":
+            dist.all_gather(list(recv.view(self.world, -1).unbind(0)), send, group=self.group)
+        else:
+            dist.all_gather_into_tensor(recv, send, group=self.group)
 
     def reset(self):
         """Start a new pass, recycling the buffer the previous pass reduced into."""

@@ -140,9 +140,9 @@ def per_sample_predictive_std(kfac, x: Tensor, layers: Iterable = None, chunk: i
     layers = list(layers)
     names = {id(p): n for n, p in model.named_parameters()}
     pnames = [[names[id(p)] for p in layer.parameters()] for layer in layers]
-    # KFAC's full backward hooks wrap outputs in an autograd.Function that functorch
-    # transforms cannot trace: suspend every module hook for this call, then restore
-    # the exact hook dictionaries
+    # KFAC's module hooks (record capture) must not fire inside the functorch
+    # transforms: suspend every module hook for this call, then restore the exact
+    # hook dictionaries
     kinds = ("_forward_hooks", "_forward_pre_hooks", "_backward_hooks", "_backward_pre_hooks")
     saved = [(m, [getattr(m, k) for k in kinds]) for m in model.modules()]
     for m, _ in saved:

@@ -238,6 +238,30 @@ KFAC_API size_t kfac_sample_workspace_bytes(const kfac_sample_job* jobs, int njo
 KFAC_API int kfac_sample(const kfac_sample_job* jobs, int njobs, int accumulate, void* workspace,
                 size_t workspace_bytes, kfac_stream_t stream);
 
+/* ------------------------------------------------- packed lower triangles
+ * For the data-parallel collectives (no reference counterpart: the reference is
+ * single-device).  Row i of a factor's lower triangle lives at
+ * packed[offset + i(i+1)/2 .. + i], so a factor takes n(n+1)/2 floats and the
+ * caller lays the factors out back to back.
+ *   kfac_tri_pack  : packed <- lower triangles of the F's (the all-reduce of the
+ *                    per-rank factor sums, curvatures.py:359-363 summed over ranks)
+ *   kfac_tri_unpack: F <- packed, upper triangle mirrored (KFAC_TRI_SYMMETRIC: the
+ *                    reduced A, G) or zeroed (KFAC_TRI_LOWER: the L_A, L_G of a
+ *                    sharded inversion, curvatures.py:391-398, after the gather). */
+enum kfac_tri_mode { KFAC_TRI_SYMMETRIC = 0, KFAC_TRI_LOWER = 1 };
+
+typedef struct kfac_tri_job {
+  float* F;
+  int64_t ldF;
+  int32_t n;
+  int32_t reserved;
+  int64_t offset; /* elements into `packed` */
+} kfac_tri_job;
+
+KFAC_API int kfac_tri_pack(const kfac_tri_job* jobs, int njobs, float* packed, kfac_stream_t stream);
+KFAC_API int kfac_tri_unpack(const kfac_tri_job* jobs, int njobs, const float* packed, int mode,
+                             kfac_stream_t stream);
+
 /* -------------------------------------------------------------- profiling
  * Optional HIP-event timing of the library's own launches, recorded on the
  * stream each kernel is launched on (off by default; not graph-capturable when

@@ -22,6 +22,13 @@ exercised are:
   `pinv(N(q+tau I)) (x) pinv(N(h+tau I))` quadratic form (G7)
 * `models/curvatures.py:400-405, 117-129, 68-82`  KFAC.sample, sample_and_replace and
   Curvature._replace on a conv (bias) + linear (no bias) net, with the z draws (G8)
+* `models/curvatures.py:295-398`  hooks + update + invert on a net with
+  nn.ReLU(inplace=True) after its layers (G9)
+* `models/curvatures.py:408-473, 476-682`  EFB and INF (update / invert / sample,
+  dim reduction, diagonal correction, pre-sampler, sampler) on injected eigenbases
+  and gradients; only get_eigenvectors (torch.symeig) is unavailable (G10/G11)
+
+Singleton functions may be run alone: `python tests/golden/make_goldens.py g9_inplace`.
 """
 import os
 import sys
@@ -354,7 +361,161 @@ def g8_sample():
     save("g8_sample.npz", **res)
 
 
+# ------------------------------------ G9 hooks with in-place activations (torchvision style)
+def g9_inplace():
+    """curvatures.py:295-365 + 367-398 end to end on a conv + linear net whose layers
+    are followed by nn.ReLU(inplace=True): the reference's legacy backward hook sees
+    dL/d(layer output) there; the records, factors and inverse factors."""
+    torch.manual_seed(4)
+    net = nn.Sequential(nn.Conv2d(1, 4, 3, padding=1), nn.ReLU(inplace=True), nn.MaxPool2d(2),
+                        nn.Flatten(), nn.Linear(64, 10), nn.ReLU(inplace=True), nn.Linear(10, 3))
+    out = {f"w_{k}": npf(v) for k, v in net.state_dict().items()}
+    kfac = KFAC(net)
+    criterion = nn.CrossEntropyLoss()
+    rng = np.random.default_rng(29)
+    layers = [net[0], net[4], net[6]]
+    for bi in range(2):
+        x = rng.random((8, 1, 8, 8), dtype=np.float32)
+        logits = net(torch.from_numpy(x))
+        labels = torch.distributions.Categorical(logits=logits).sample()
+        loss = criterion(logits, labels)
+        net.zero_grad()
+        loss.backward()
+        for li, layer in enumerate(layers):
+            out[f"rec{bi}_a{li}"] = npf(kfac.record[layer][0])
+            out[f"rec{bi}_g{li}"] = npf(kfac.record[layer][1])
+        kfac.update(batch_size=8)
+        out[f"x{bi}"], out[f"y{bi}"] = x, npf(labels)
+    for li, layer in enumerate(layers):
+        out[f"A{li}"], out[f"G{li}"] = npf(kfac.state[layer][0]), npf(kfac.state[layer][1])
+    kfac.invert(0.2 ** 2, 200)
+    for li, layer in enumerate(layers):
+        LA, LG = kfac.inv_state[layer]
+        out[f"LA{li}"], out[f"LG{li}"] = npf(LA), npf(LG)
+    save("g9_inplace.npz", **out)
+
+
+# ------------------------------------------------------------- G10 EFB, G11 INF
+def _no_init(cls, net, **attrs):
+    """A reference EFB/INF instance without __init__: its get_eigenvectors calls
+    torch.symeig, removed in torch 2.0, so the eigenbases are injected (eigh of
+    F + F^T, symeig's successor); every other attribute is what Curvature.__init__
+    sets (curvatures.py:38-65)."""
+    import copy
+    obj = cls.__new__(cls)
+    obj.model = net
+    obj.model_state = copy.deepcopy(net.state_dict())
+    obj.layer_types = ['Linear', 'Conv2d', 'MultiheadAttention']
+    obj.state = dict()
+    obj.inv_state = dict()
+    for k, v in attrs.items():
+        setattr(obj, k, v)
+    return obj
+
+
+def g10_g11_efb_inf():
+    """EFB (curvatures.py:408-473) and INF (:476-682) run by the reference on injected
+    eigenbases and gradients: lambdas, diags, inverses, samples (with their draws),
+    INF's dim reduction, diagonal correction and pre-sample."""
+    from models.curvatures import EFB, INF
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Conv2d(1, 3, 3), nn.ReLU(), nn.Flatten(), nn.Linear(3 * 4 * 4, 4))
+    layers = [net[0], net[3]]
+    rng = np.random.default_rng(31)
+    kfac = KFAC(net)
+    for _ in range(2):
+        x = torch.from_numpy(rng.random((32, 1, 6, 6), dtype=np.float32))
+        net.zero_grad()
+        F.cross_entropy(net(x), torch.from_numpy(rng.integers(0, 4, 32))).backward()
+        kfac.update(batch_size=32)
+    out = {}
+    eigvecs = {}
+    for li, layer in enumerate(layers):
+        A, G = kfac.state[layer]
+        out[f"A{li}"], out[f"G{li}"] = npf(A), npf(G)
+        V_A = torch.linalg.eigh(A + A.t())[1]
+        V_G = torch.linalg.eigh(G + G.t())[1]
+        eigvecs[layer] = (V_A, V_G)
+        out[f"VA{li}"], out[f"VG{li}"] = npf(V_A), npf(V_G)
+    efb = _no_init(EFB, net, eigvecs=eigvecs, diags=dict())
+    for u in range(3):
+        for li, layer in enumerate(layers):
+            gw = rng.standard_normal(tuple(layer.weight.shape), dtype=np.float32) * 0.1
+            gb = rng.standard_normal(tuple(layer.bias.shape), dtype=np.float32) * 0.1
+            layer.weight.grad = torch.from_numpy(gw)
+            layer.bias.grad = torch.from_numpy(gb)
+            out[f"gw{u}_{li}"], out[f"gb{u}_{li}"] = gw, gb
+        efb.update(batch_size=32)
+    for li, layer in enumerate(layers):
+        out[f"efb_lambda{li}"] = npf(efb.state[layer])
+        out[f"efb_diag{li}"] = npf(efb.diags[layer])
+    efb.invert(0.04, 200.0)
+    for li, layer in enumerate(layers):
+        out[f"efb_inv{li}"] = npf(efb.inv_state[layer])
+        torch.manual_seed(5 + li)
+        out[f"efb_sample{li}"] = npf(efb.sample(layer))
+        torch.manual_seed(5 + li)
+        out[f"efb_z{li}"] = npf(torch.randn(eigvecs[layer][0].shape[0], eigvecs[layer][1].shape[0]))
+    # INF through the reference's own update/invert/sample at full rank (its
+    # _dim_reduction passes everything through there, curvatures.py:631-632)
+    inf = _no_init(INF, net, eigvecs=eigvecs, lambdas=efb.state, diags=efb.diags)
+    inf.update(rank=10 ** 6)
+    for li, layer in enumerate(layers):
+        for k, t in zip(("U_A", "U_G", "lr_lambda", "correction"), inf.state[layer]):
+            out[f"inf_{k}{li}"] = npf(t)
+    inf.invert(0.04, 200.0)
+    for li, layer in enumerate(layers):
+        for k, t in zip(("inv_U_A", "inv_U_G", "reg_inv_correction", "pre_sample"),
+                        inf.inv_state[layer]):
+            out[f"inf_{k}{li}"] = npf(t)
+        torch.manual_seed(9 + li)
+        out[f"inf_sample{li}"] = npf(inf.sample(layer))
+        torch.manual_seed(9 + li)
+        out[f"inf_X{li}"] = npf(torch.randn(eigvecs[layer][0].shape[0] * eigvecs[layer][1].shape[0]))
+    # rank < n: the reference's _dim_reduction raises at its final gather
+    # (`lambda_vec[[idx - 1 for idx in idx_top_lm]]`, curvatures.py:653: a list of 0-d
+    # tensors is a multi-dimensional index), so the fixture records that outcome and
+    # pins the rest of the reduced path -- _diagonal_accumulator, pre_sampler,
+    # sampler, run by the reference on the rows/columns its index arithmetic
+    # (curvatures.py:634-650) selects, restated here
+    rank = 6
+    inf2 = _no_init(INF, net, eigvecs=eigvecs, lambdas=efb.state, diags=efb.diags)
+    try:
+        inf2.update(rank=rank)
+        out["inf_reduced_outcome"] = np.array("ok")
+    except Exception as e:
+        out["inf_reduced_outcome"] = np.array(type(e).__name__)
+    for li, layer in enumerate(layers):
+        V_A, V_G = eigvecs[layer]
+        lam = efb.state[layer].t().contiguous().view(-1)
+        diag = efb.diags[layer].t().contiguous().view(-1)
+        m = V_G.shape[1]
+        top = (torch.argsort(-torch.abs(lam)) + 1)[:rank]  # 1-based, as the reference
+        left = torch.unique(torch.tensor([int((t - 1.) / m + 1.) for t in top]))
+        right = torch.unique(torch.tensor([int(t - m * (int((t - 1.) / m + 1.) - 1)) for t in top]))
+        flat = [int(m * (l - 1) + r) - 1 for l in left for r in right]
+        a, b, lr = V_A[:, left - 1], V_G[:, right - 1], lam[flat]
+        corr = diag - INF._diagonal_accumulator(a, b, lr)
+        corr[corr < 0] = 0
+        reg_lr = (200.0 * lr).sqrt()
+        c = torch.reciprocal(200.0 * corr + 0.04).sqrt()
+        P = INF.pre_sampler(a, b, reg_lr, c)
+        torch.manual_seed(19 + li)
+        smp = INF.sampler(a, b, c, P).reshape(a.shape[0], b.shape[0]).t()
+        torch.manual_seed(19 + li)
+        X = torch.randn(a.shape[0] * b.shape[0])
+        out.update({f"infr_left{li}": npf(left - 1), f"infr_right{li}": npf(right - 1),
+                    f"infr_lr_lambda{li}": npf(lr), f"infr_correction{li}": npf(diag - INF._diagonal_accumulator(a, b, lr)),
+                    f"infr_reg_inv_correction{li}": npf(c), f"infr_pre_sample{li}": npf(P),
+                    f"infr_sample{li}": npf(smp), f"infr_X{li}": npf(X)})
+    save("g10_efb_inf.npz", **out)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1:
+        for name in sys.argv[1:]:
+            globals()[name]()
+        sys.exit(0)
     g0_kron()
     g1_small_linear()
     g1_mlp()
@@ -363,3 +524,5 @@ if __name__ == "__main__":
     g5_g6_basenet()
     g7_regression()
     g8_sample()
+    g9_inplace()
+    g10_g11_efb_inf()

@@ -73,3 +73,69 @@ def install(monkeypatch):
     monkeypatch.setattr(N, "factor_update", fake_factor_update)
     monkeypatch.setattr(N, "factor_accum_plan", fake_accum_plan)
     monkeypatch.setattr(N, "factor_flush", fake_factor_flush)
+
+
+def _tri_rows(n):
+    return [(i, i * (i + 1) // 2) for i in range(n)]
+
+
+def fake_tri_pack(jobs, packed):
+    """kfac_tri_pack on host memory."""
+    P = packed.numpy() if hasattr(packed, "numpy") else packed
+    for j in jobs:
+        F = _view(j.F, j.n * j.ldF).reshape(j.n, j.ldF) if j.n else None
+        for i, off in _tri_rows(j.n):
+            P[j.offset + off:j.offset + off + i + 1] = F[i, :i + 1]
+
+
+def fake_tri_unpack(jobs, packed, mode):
+    """kfac_tri_unpack on host memory (mode 0 mirrors, 1 zeroes the upper triangle)."""
+    P = packed.numpy() if hasattr(packed, "numpy") else packed
+    for j in jobs:
+        F = _view(j.F, j.n * j.ldF).reshape(j.n, j.ldF) if j.n else None
+        for i, off in _tri_rows(j.n):
+            F[i, :i + 1] = P[j.offset + off:j.offset + off + i + 1]
+            if mode == 0:
+                F[:i, i] = F[i, :i]
+            else:
+                F[i, i + 1:j.n] = 0.0
+
+
+def fake_invert(jobs, device, inputs_read=None):
+    """kfac_invert (OUT_INV_CHOL): L = cholesky(inv(scale (F+F^T)/2 + shift I)) in fp64;
+    info = 1 for a factor that is not positive definite."""
+    import torch
+    info = []
+    for j in jobs:
+        F = _view(j.F, j.n * j.ldF).reshape(j.n, j.ldF)[:, :j.n].astype(np.float64)
+        R = j.scale * (F + F.T) / 2 + j.shift * np.eye(j.n)
+        out = _view(j.out, j.n * j.ldo).reshape(j.n, j.ldo)
+        try:
+            out[:, :j.n] = np.linalg.cholesky(np.linalg.inv(R)).astype(np.float32)
+            info.append(0)
+        except np.linalg.LinAlgError:
+            info.append(1)
+    return torch.tensor(info, dtype=torch.int32)
+
+
+class HostEvent:
+    def query(self):
+        return True
+
+    def synchronize(self):
+        pass
+
+
+def install_distributed(kfac=None):
+    """Host doubles for the collectives' device kernels (and the sharded inversion's
+    verdict readback on `kfac`)."""
+    from bnn_kfac_amd import _native as N
+    N.require_device = lambda t, what, owner=None: None
+    N.factor_update = fake_factor_update
+    N.factor_accum_plan = fake_accum_plan
+    N.factor_flush = fake_factor_flush
+    N.tri_pack = fake_tri_pack
+    N.tri_unpack = fake_tri_unpack
+    N.invert = fake_invert
+    if kfac is not None:
+        kfac._readback = lambda info: (HostEvent(), info.clone())

@@ -27,15 +27,12 @@ def _worker(rank, world, port, result_q, scenario):
         import sys
         sys.path.insert(0, os.path.dirname(__file__))
         import host_double
-        from bnn_kfac_amd import _native as N
         from bnn_kfac_amd.distributed import DistributedKFAC
-        N.require_device = lambda t, what, owner=None: None
-        N.factor_update = host_double.fake_factor_update
-        N.factor_accum_plan = host_double.fake_accum_plan
-        N.factor_flush = host_double.fake_factor_flush
+        host_double.install_distributed()
         torch.manual_seed(0)
         net = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.ReLU(), torch.nn.Linear(5, 3))
         kfac = DistributedKFAC(net)
+        host_double.install_distributed(kfac)
         calls = {"n": 0}
         orig = dist.all_reduce
 
@@ -59,10 +56,25 @@ def _worker(rank, world, port, result_q, scenario):
                 kfac.record[net[0]] = [torch.from_numpy(A1[sl]), torch.from_numpy(G1[sl])]
                 kfac.record[net[2]] = [torch.from_numpy(A2[sl]), torch.from_numpy(G2[sl])]
                 kfac.update(cut[1] - cut[0], global_batch_size=gb)
-            kfac.allreduce()
+            if scenario == "state_read":
+                kfac.state  # a state read completes the pass (collective on every rank)
+            else:
+                kfac.allreduce()
         dist.all_reduce = orig
         out = [t.numpy().copy() for pair in kfac.state.values() for t in pair]
-        result_q.put((rank, out, calls["n"]))
+        inv = None
+        if scenario in ("sharded", "sharded_singular"):
+            if scenario == "sharded_singular":
+                # layer 1's G made indefinite: layers from the first failing one are
+                # dropped and LinAlgError raised on every rank (curvatures.py:393-396)
+                kfac.state[net[2]][1].fill_(-1.0)
+            kfac.shard_inversion = True
+            try:
+                kfac.invert(0.04, 200)
+                inv = [t.numpy().copy() for pair in kfac.inv_state.values() for t in pair]
+            except np.linalg.LinAlgError:
+                inv = ("LinAlgError", sorted(kfac._inv_state.keys(), key=id) == sorted([net[0]], key=id))
+        result_q.put((rank, out, calls["n"], inv))
     finally:
         dist.destroy_process_group()
 
@@ -86,7 +98,8 @@ def _reference(scenario):
 
 
 @pytest.mark.parametrize("scenario,world", [("even", 2), ("uneven", 2), ("two_passes", 2),
-                                            ("even", 4)])
+                                            ("even", 4), ("state_read", 2), ("sharded", 2),
+                                            ("sharded", 3), ("sharded_singular", 2)])
 def test_sharded_pass_matches_single_device(scenario, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -99,8 +112,16 @@ def test_sharded_pass_matches_single_device(scenario, world):
         p.join(timeout=60)
         assert p.exitcode == 0
     want = _reference(scenario)
-    for rank, got, n_allreduce in results:
+    for rank, got, n_allreduce, inv in results:
         # one packed all-reduce per pass (two_passes: two)
         assert n_allreduce == (2 if scenario == "two_passes" else 1)
         for g, w in zip(got, want):
             np.testing.assert_allclose(g, w, rtol=1e-5, atol=1e-6)
+        if scenario == "sharded":
+            # every rank holds every L factor (its own inverted, the rest gathered)
+            from oracle import kfac_oracle as O
+            for g, F in zip(inv, got):
+                np.testing.assert_allclose(g, O.invert_factor(F.astype(np.float64), 0.04, 200),
+                                           rtol=1e-5, atol=1e-6)
+        if scenario == "sharded_singular":
+            assert inv == ("LinAlgError", True)

@@ -1,0 +1,117 @@
+"""CPU: the oracle and the host-side logic against fixtures made by the reference itself.
+
+* G9 (tests/golden/g9_inplace.npz): a conv + linear net with nn.ReLU(inplace=True)
+  after its layers, run through the reference's hooks (curvatures.py:295-323) and
+  update/invert (:325-398).  KFAC's hooks here must record what the reference's
+  legacy backward hook records (dL/d(layer output), before the in-place ReLU), and
+  the oracle on those records must give the reference's factors.
+* G10/G11 (g10_efb_inf.npz): the reference's EFB (curvatures.py:408-473) and INF
+  (:476-682) on injected eigenbases and gradients.  INF's rank reduction raises in
+  the reference itself (curvatures.py:653); its remaining steps are pinned on the
+  rows/columns the reference's index arithmetic selects.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from conftest import golden
+from oracle import kfac_oracle as O
+
+
+def _g9_net():
+    net = nn.Sequential(nn.Conv2d(1, 4, 3, padding=1), nn.ReLU(inplace=True), nn.MaxPool2d(2),
+                        nn.Flatten(), nn.Linear(64, 10), nn.ReLU(inplace=True), nn.Linear(10, 3))
+    g = golden("g9_inplace.npz")
+    net.load_state_dict({k[2:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("w_")})
+    return net, g
+
+
+def test_g9_hooks_with_inplace_relu_record_like_the_reference():
+    from bnn_kfac_amd.curvatures import KFAC
+    net, g = _g9_net()
+    kfac = KFAC(net)
+    layers = [net[0], net[4], net[6]]
+    ref = O.OracleKFAC(np.float64)
+    for bi in range(2):
+        logits = net(torch.from_numpy(g[f"x{bi}"]))
+        loss = nn.functional.cross_entropy(logits, torch.from_numpy(g[f"y{bi}"]))
+        net.zero_grad()
+        loss.backward()  # raised with a full backward hook + ReLU(inplace=True)
+        for li, layer in enumerate(layers):
+            a, gr = (t.detach().numpy() for t in kfac.record[layer])
+            np.testing.assert_array_equal(a, g[f"rec{bi}_a{li}"])
+            np.testing.assert_allclose(gr, g[f"rec{bi}_g{li}"], rtol=1e-6, atol=1e-7)
+        ref.update_conv("c", kfac.record[net[0]][0].detach().numpy(),
+                        kfac.record[net[0]][1].detach().numpy(), (3, 3), (1, 1), (1, 1), True)
+        for name, layer in (("f1", net[4]), ("f2", net[6])):
+            ref.update_linear(name, kfac.record[layer][0].detach().numpy(),
+                              kfac.record[layer][1].detach().numpy(), True)
+    for li, name in enumerate(("c", "f1", "f2")):
+        A, G = ref.state[name]
+        np.testing.assert_allclose(A, g[f"A{li}"], rtol=1e-5, atol=1e-6 * np.abs(g[f"A{li}"]).max())
+        np.testing.assert_allclose(G, g[f"G{li}"], rtol=1e-5, atol=1e-6 * np.abs(g[f"G{li}"]).max())
+        for F, L in ((g[f"A{li}"], g[f"LA{li}"]), (g[f"G{li}"], g[f"LG{li}"])):
+            want = O.invert_factor(F.astype(np.float64), 0.04, 200)
+            np.testing.assert_allclose(L, want, rtol=0, atol=1e-4 * np.abs(want).max())
+
+
+@pytest.mark.parametrize("li", [0, 1])
+def test_g10_efb_oracle_vs_reference(li):
+    g = golden("g10_efb_inf.npz")
+    VA, VG = g[f"VA{li}"], g[f"VG{li}"]
+    grads = [np.concatenate([g[f"gw{u}_{li}"].reshape(g[f"gw{u}_{li}"].shape[0], -1),
+                             g[f"gb{u}_{li}"][:, None]], 1) for u in range(3)]
+    lam = sum(O.efb_lambdas(gr, VA, VG) for gr in grads)
+    np.testing.assert_allclose(lam, g[f"efb_lambda{li}"], rtol=1e-4, atol=1e-6 * lam.max())
+    np.testing.assert_allclose(sum(gr.astype(np.float64) ** 2 * 32 for gr in grads),
+                               g[f"efb_diag{li}"], rtol=1e-6)
+    inv = O.efb_invert(g[f"efb_lambda{li}"], 0.04, 200.0)
+    np.testing.assert_allclose(inv, g[f"efb_inv{li}"], rtol=1e-6)
+    s = O.efb_sample(VA, VG, g[f"efb_inv{li}"], g[f"efb_z{li}"])
+    np.testing.assert_allclose(s, g[f"efb_sample{li}"], rtol=1e-4, atol=1e-5 * np.abs(s).max())
+
+
+@pytest.mark.parametrize("li", [0, 1])
+def test_g11_inf_host_algebra_vs_reference(li):
+    """INF's torch restatements (the product's host algebra; CPU here) and the
+    literal oracle against the reference's own INF outputs."""
+    from bnn_kfac_amd.curvatures import INF
+    g = golden("g10_efb_inf.npz")
+    assert str(g["inf_reduced_outcome"]) == "IndexError"  # the reference's rank < n path
+    VA, VG = (torch.from_numpy(g[k]) for k in (f"VA{li}", f"VG{li}"))
+    lam = torch.from_numpy(g[f"efb_lambda{li}"]).t().contiguous().view(-1)
+    diag = torch.from_numpy(g[f"efb_diag{li}"]).t().contiguous().view(-1)
+    # full rank: the reference's update -> invert -> sample
+    a, b, lr = INF._dim_reduction(VA, VG, lam, 10 ** 6)
+    corr = diag - INF._diagonal_accumulator(a, b, lr)
+    tol = 1e-5 * float(diag.abs().max())
+    np.testing.assert_allclose(corr.numpy(), g[f"inf_correction{li}"], rtol=1e-5, atol=tol)
+    corr[corr < 0] = 0
+    c = torch.reciprocal(200.0 * corr + 0.04).sqrt()
+    np.testing.assert_allclose(c.numpy(), g[f"inf_reg_inv_correction{li}"], rtol=1e-4)
+    c = torch.from_numpy(g[f"inf_reg_inv_correction{li}"])
+    P = INF.pre_sampler(a.double(), b.double(), (200.0 * lr.double()).sqrt(), c.double()).numpy()
+    want = g[f"inf_pre_sample{li}"]
+    # the reference's fp32 pre-sample is itself ~5e-4 off the fp64 truth (V_s^T V_s is
+    # ill-conditioned at full rank): compared normwise at 2e-3
+    np.testing.assert_allclose(P, want, rtol=0, atol=2e-3 * np.abs(want).max())
+    s = O.inf_sampler(a.numpy(), b.numpy(), c.numpy(), want, g[f"inf_X{li}"])
+    s = s.reshape(a.shape[0], b.shape[0]).T
+    np.testing.assert_allclose(s, g[f"inf_sample{li}"], rtol=1e-4, atol=1e-4 * np.abs(s).max())
+    # rank 6: the reference's index arithmetic (curvatures.py:634-650) and the rest
+    a, b, lr = INF._dim_reduction(VA, VG, lam, 6)
+    wa, wb, wl = O.inf_dim_reduction(VA.numpy(), VG.numpy(), lam.numpy(), 6)
+    np.testing.assert_array_equal(a.numpy(), VA.numpy()[:, g[f"infr_left{li}"]])
+    np.testing.assert_array_equal(b.numpy(), VG.numpy()[:, g[f"infr_right{li}"]])
+    np.testing.assert_array_equal(lr.numpy(), g[f"infr_lr_lambda{li}"])
+    np.testing.assert_array_equal(wl, g[f"infr_lr_lambda{li}"])
+    corr = diag - INF._diagonal_accumulator(a, b, lr)
+    np.testing.assert_allclose(corr.numpy(), g[f"infr_correction{li}"], rtol=1e-5, atol=tol)
+    c = torch.from_numpy(g[f"infr_reg_inv_correction{li}"])
+    P = INF.pre_sampler(a, b, (200.0 * lr).sqrt(), c).numpy()
+    want = g[f"infr_pre_sample{li}"]
+    np.testing.assert_allclose(P, want, rtol=0, atol=1e-4 * np.abs(want).max())
+    s = O.inf_sampler(a.numpy(), b.numpy(), c.numpy(), want, g[f"infr_X{li}"])
+    s = s.reshape(a.shape[0], b.shape[0]).T
+    np.testing.assert_allclose(s, g[f"infr_sample{li}"], rtol=1e-4, atol=1e-4 * np.abs(s).max())

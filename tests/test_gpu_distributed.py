@@ -1,7 +1,17 @@
-"""GPU, world_size 2 on one device (gloo carries the collective; RCCL cannot put two
-ranks on one GPU): the data-parallel factor pass with the real HIP kernels reproduces
-single-device KFAC — same factors (one packed all-reduce per pass) and the same
-inverse Cholesky factors — over two passes with an uneven last batch."""
+"""GPU, data-parallel KFAC with the real HIP kernels (models/curvatures.py:359-363 summed
+over ranks):
+
+* world 2 on one device (gloo carries the collective; RCCL cannot put two ranks on
+  one GPU): the sharded pass reproduces single-device KFAC -- same factors (ONE
+  packed-lower-triangle all-reduce per pass) and the same inverse Cholesky factors --
+  over two passes with an uneven last batch; at C4's per-rank shape (8,192 rows per
+  rank of a 16,384-row global batch); and with the inversion sharded over the ranks
+  (each inverts its factors, one all-gather of the packed L triangles + verdicts);
+* RCCL itself: a world-1 "nccl" process group running the same collectives
+  (DistributedKFAC.always_reduce), so the RCCL all-reduce / all-gather path runs
+  on the box;
+* kfac_tri_pack / kfac_tri_unpack round trips, bit-exact.
+"""
 import os
 import socket
 
@@ -13,7 +23,7 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
-SIZES = (512, 512, 300)  # global batches; the last one splits unevenly over 2 ranks
+SIZES = {"small": ((512, 512, 300), 2), "c4": ((16384, 16384), 1)}  # global batches, passes
 
 
 def _free_port():
@@ -22,10 +32,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _data():
+def _data(shape):
     rng = np.random.default_rng(7)
     out = []
-    for gb in SIZES:
+    for gb in SIZES[shape][0]:
         out.append((rng.random((gb, 784), dtype=np.float32),
                     rng.standard_normal((gb, 128)).astype(np.float32),
                     rng.random((gb, 128), dtype=np.float32),
@@ -39,20 +49,26 @@ def _net(dev):
                                torch.nn.Linear(128, 10)).to(dev)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, shape, shard, backend):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from bnn_kfac_amd.distributed import DistributedKFAC
-        dev = torch.device("cuda:0")
         net = _net(dev)
-        kfac = DistributedKFAC(net)
-        for p in range(2):
+        kfac = DistributedKFAC(net, shard_inversion=shard)
+        kfac.always_reduce = True
+        for p in range(SIZES[shape][1]):
             kfac.reset()
-            for a1, g1, a2, g2 in _data():
+            for a1, g1, a2, g2 in _data(shape):
                 gb = a1.shape[0]
-                cut = [0, gb // 2 + 37, gb][rank:rank + 2]  # uneven shards
+                cut = [0, gb // 2 + (37 if shape == "small" else 0), gb][rank:rank + 2] if world == 2 \
+                    else [0, gb]
                 sl = slice(*cut)
                 kfac.record[net[0]] = [torch.from_numpy(a1[sl]).to(dev), torch.from_numpy(g1[sl]).to(dev)]
                 kfac.record[net[2]] = [torch.from_numpy(a2[sl]).to(dev), torch.from_numpy(g2[sl]).to(dev)]
@@ -60,38 +76,85 @@ def _worker(rank, world, port, q):
             kfac.invert(0.04, 200)
         st = [t.cpu().numpy() for pair in kfac.state.values() for t in pair]
         inv = [t.cpu().numpy() for pair in kfac.inv_state.values() for t in pair]
-        q.put((rank, st, inv))
+        q.put((rank, st, inv, kfac._sharded_last))
     finally:
         dist.destroy_process_group()
 
 
-def test_two_ranks_match_single_device(hip_device):
+def _single_device(dev, shape):
     from bnn_kfac_amd.curvatures import KFAC
+    net = _net(dev)
+    kfac = KFAC(net)
+    for a1, g1, a2, g2 in _data(shape):
+        kfac.record[net[0]] = [torch.from_numpy(a1).to(dev), torch.from_numpy(g1).to(dev)]
+        kfac.record[net[2]] = [torch.from_numpy(a2).to(dev), torch.from_numpy(g2).to(dev)]
+        kfac.update(a1.shape[0])
+    kfac.invert(0.04, 200)
+    return ([t.cpu().numpy() for pair in kfac.state.values() for t in pair],
+            [t.cpu().numpy() for pair in kfac.inv_state.values() for t in pair])
+
+
+def _run(world, shape, shard, backend="gloo"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, shape, shard, backend))
+             for r in range(world)]
     for p in procs:
         p.start()
     results = sorted([q.get(timeout=300) for _ in procs], key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    net = _net(hip_device)
-    kfac = KFAC(net)
-    for a1, g1, a2, g2 in _data():
-        kfac.record[net[0]] = [torch.from_numpy(a1).to(hip_device), torch.from_numpy(g1).to(hip_device)]
-        kfac.record[net[2]] = [torch.from_numpy(a2).to(hip_device), torch.from_numpy(g2).to(hip_device)]
-        kfac.update(a1.shape[0])
-    kfac.invert(0.04, 200)
-    want_st = [t.cpu().numpy() for pair in kfac.state.values() for t in pair]
-    want_inv = [t.cpu().numpy() for pair in kfac.inv_state.values() for t in pair]
-    for rank, st, inv in results:
+    return results
+
+
+def _check(results, want_st, want_inv, shard):
+    for rank, st, inv, sharded in results:
+        assert sharded == bool(shard)
         for g, w in zip(st, want_st):
             np.testing.assert_allclose(g, w, rtol=1e-5, atol=1e-5 * np.abs(w).max())
-        # replicated inversion of the reduced factors: the sharded sums differ from the
-        # single-device ones in the last bits, which the inversion amplifies by cond(R)
-        # (~1e5 here) -> normwise 1e-4 (the north-star tolerance)
+        # the reduced factors differ from the single-device sums in the last bits,
+        # which the inversion amplifies by cond(R) (~1e5 here) -> normwise 1e-4 (the
+        # north-star tolerance)
         for g, w in zip(inv, want_inv):
             np.testing.assert_allclose(g, w, rtol=0, atol=1e-4 * np.abs(w).max())
-    np.testing.assert_array_equal(results[0][2][0], results[1][2][0])  # ranks agree exactly
+            assert np.all(np.triu(g, 1) == 0)
+    for a, b in zip(results[0][2], results[-1][2]):  # every rank holds the same L factors
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("shape,shard", [("small", False), ("c4", False), ("small", True)])
+def test_two_ranks_match_single_device(hip_device, shape, shard):
+    results = _run(2, shape, shard)
+    want_st, want_inv = _single_device(hip_device, shape)
+    _check(results, want_st, want_inv, shard)
+
+
+@pytest.mark.parametrize("shard", [False, True])
+def test_rccl_world1_collectives(hip_device, shard):
+    """The RCCL (nccl backend) all-reduce of the packed triangles and, sharded, the
+    all-gather of the L factors, at world 1: results equal plain KFAC's."""
+    results = _run(1, "small", shard, backend="nccl")
+    want_st, want_inv = _single_device(hip_device, "small")
+    _check(results, want_st, want_inv, shard)
+
+
+@pytest.mark.parametrize("sizes", [(1, 10, 64, 65), (785, 128, 129, 10), (4097, 33)])
+def test_tri_pack_unpack_roundtrip(hip_device, sizes):
+    from bnn_kfac_amd import _native as N
+    rng = np.random.default_rng(sum(sizes))
+    mats = [torch.from_numpy(rng.standard_normal((n, n)).astype(np.float32)).to(hip_device)
+            for n in sizes]
+    jobs, total = N.tri_jobs(mats)
+    packed = torch.full((total,), float("nan"), device=hip_device)
+    N.tri_pack(jobs, packed)
+    want = np.concatenate([m.cpu().numpy()[np.tril_indices(m.shape[0])] for m in mats])
+    np.testing.assert_array_equal(packed.cpu().numpy(), want)
+    for mode in (N.TRI_SYMMETRIC, N.TRI_LOWER):
+        outs = [torch.full_like(m, float("nan")) for m in mats]
+        N.tri_unpack(N.tri_jobs(outs)[0], packed, mode)
+        for m, o in zip(mats, outs):
+            low = np.tril(m.cpu().numpy())
+            exp = low + np.tril(low, -1).T if mode == N.TRI_SYMMETRIC else low
+            np.testing.assert_array_equal(o.cpu().numpy(), exp)

@@ -35,12 +35,12 @@ def test_gfx950_code_object_present():
 
 
 @pytest.mark.parametrize("name", ["kfac_operand", "kfac_factor_job", "kfac_invert_job",
-                                  "kfac_eig_job", "kfac_quad_job"])
+                                  "kfac_eig_job", "kfac_quad_job", "kfac_tri_job"])
 def test_struct_layout_matches_header(tmp_path, name):
     from bnn_kfac_amd import _native as N
     pyname = {"kfac_operand": "Operand", "kfac_factor_job": "FactorJob",
               "kfac_invert_job": "InvertJob", "kfac_eig_job": "EigJob",
-              "kfac_quad_job": "QuadJob"}[name]
+              "kfac_quad_job": "QuadJob", "kfac_tri_job": "TriJob"}[name]
     c = tmp_path / "sz.c"
     c.write_text(f'#include <stdio.h>\n#include "{HEADER}"\n'
                  f'int main(void){{printf("%zu", sizeof({name})); return 0;}}\n')
