@@ -242,6 +242,10 @@ def main(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-serial", action="store_true")
+    ap.add_argument("--launch-first", type=int, default=None,
+                    help="queued updates in a pass's first SYRK launch (KFAC.launch_first)")
+    ap.add_argument("--launch-idle", action="store_true",
+                    help="KFAC.launch_policy = 'idle' (launch when the stream drains)")
     ap.add_argument("--partition", type=int, default=0,
                     help="CUs reserved for the overlapped inversion (KFAC.partition_cus; 0 = none)")
     argv = sys.argv[1:] if argv is None else argv
@@ -285,6 +289,10 @@ def main(argv=None):
     layers = [m for m in net.modules() if isinstance(m, (torch.nn.Linear, torch.nn.Conv2d))]
     kfac = DistributedKFAC(net) if world > 1 else KFAC(net)
     kfac.partition_cus = args.partition
+    if args.launch_first:
+        kfac.launch_first = args.launch_first
+    if args.launch_idle:
+        kfac.launch_policy = "idle"
     recs = synthetic_records(specs, images, device, seed=1234 + rank)
     starts = list(range(0, images, batch))
     comm = {"ms": 0.0, "n": 0, "timing": False}

@@ -187,9 +187,19 @@ class KFAC(Curvature):
         #   once, when the state is next read (invert / save / `state` / all-reduce).
         self.defer_reduce = True
         self.defer_batches = 64
+        # queued updates keep their records alive until their launch (the reference
+        # frees them after each update): the queue is also launched once the records
+        # it holds reach this many bytes, so a wide or conv model's activations are
+        # not retained beyond ~this much (MLP batch of 4096: 17 MB per update)
+        self.defer_bytes = 256 << 20
+        self._queue_bytes = 0
         self._queue = []         # per queued update: (jobs, operand pointers, kept records,
                                  # their _version, device, merge key)
-        self._launch_at = 1      # queue length that triggers the next launch
+        # launch sizes: the first launch of a pass takes `launch_first` queued updates,
+        # each later one twice as many (up to defer_batches)
+        self.launch_first = 1
+        self.launch_policy = "double"
+        self._launch_at = self.launch_first  # queue length that triggers the next launch
         self._fast = None        # job templates of the last slow-path update (see _remember)
         self._acc_buf = None     # device buffer of the accumulators
         self._acc_map = None     # F pointer -> (acc pointer, splits) of the pending cycle
@@ -228,7 +238,8 @@ class KFAC(Curvature):
             self._cycle_stream = None
             self._cycle_hold = []
         self._queue = []
-        self._launch_at = 1
+        self._queue_bytes = 0
+        self._launch_at = self.launch_first
         self._fast = None
         self._acc_flush = self._acc_map = None
         self._state = dict()
@@ -239,7 +250,7 @@ class KFAC(Curvature):
         factors (async; one reduce launch)."""
         if getattr(self, "_queue", None):
             self._launch_queue()
-        self._launch_at = 1
+        self._launch_at = getattr(self, "launch_first", 1)
         jobs = getattr(self, "_acc_flush", None)
         if jobs:
             self._acc_flush = self._acc_map = None
@@ -494,12 +505,31 @@ class KFAC(Curvature):
         if self._queue and self._queue[0][4] != entry[4]:
             self._launch_queue()
         self._queue.append(entry)
-        # launch sizes double from 1 up to defer_batches: the first update of a pass
-        # goes to the GPU at once, and while a launch runs the host queues the next,
-        # twice as large one (a pass of 15 updates: 5 launches, not 15)
-        if len(self._queue) >= min(self._launch_at, max(1, self.defer_batches)):
+        self._queue_bytes += sum(t.numel() * t.element_size() for t in entry[2])
+        # launch policy (the records held are capped by defer_bytes either way):
+        # * "double" (default): launch sizes double from `launch_first` up to
+        #   defer_batches -- a function of the update count only, so the launches'
+        #   K-splits, and with them the factors' fp32 summation order, are the same
+        #   on every run;
+        # * "idle": launch as soon as the caller's stream has drained, else keep
+        #   queueing (a pipelined pass becomes one or two large launches, ~2 % more
+        #   images/s on the MLP bench), but the grouping then follows GPU timing and
+        #   the factors can differ in their last bits from run to run.
+        if len(self._queue) >= max(1, self.defer_batches) or self._queue_bytes >= self.defer_bytes:
+            self._launch_queue()
+        elif self.launch_policy == "idle":
+            if self._stream_idle(entry[4]):
+                self._launch_queue()
+        elif len(self._queue) >= self._launch_at:
             self._launch_at *= 2
             self._launch_queue()
+
+    def _stream_idle(self, device):
+        """True when every launch on the caller's stream (and the cycle's) has run."""
+        if device.type != "cuda":  # (the host test double runs on the CPU)
+            return True
+        stream = self._cycle_stream or torch.cuda.current_stream(device)
+        return stream.query()
 
     def _launch_queue(self):
         """Launch the queued updates: consecutive updates with the same job templates
@@ -507,6 +537,7 @@ class KFAC(Curvature):
         (channel-major / im2col jobs, already B*Ho*Wo rows of K each, stay one job
         per batch)."""
         queue, self._queue = self._queue, []
+        self._queue_bytes = 0
         for _jobs, _ptrs, keep, versions, _dev, _key in queue:
             for t, v in zip(keep, versions):
                 if t._version != v:

@@ -162,11 +162,12 @@ def test_queued_updates_merge_into_multibatch_jobs(monkeypatch):
                 torch.tensor(rng.standard_normal((B, 3)).astype(np.float32))]
                for B in sizes]
 
-    def run(defer_reduce, defer_batches=64):
+    def run(defer_reduce, defer_batches=64, defer_bytes=256 << 20):
         host_double.UPDATES.clear()
         net = mlp()
         kfac = KFAC(net)
         kfac.defer_reduce, kfac.defer_batches = defer_reduce, defer_batches
+        kfac.defer_bytes = defer_bytes
         for a1, g1, a2, g2 in batches:
             kfac.record[net[0]] = [a1, g1]
             kfac.record[net[2]] = [a2, g2]
@@ -182,6 +183,12 @@ def test_queued_updates_merge_into_multibatch_jobs(monkeypatch):
         np.testing.assert_allclose(g, w, rtol=1e-6)
     got, launches = run(True, defer_batches=2)  # [8] [8 8] [5 8] [8]
     assert launches == [[1] * 4, [2] * 4, [1] * 4, [1] * 4, [1] * 4]
+    for g, w in zip(got, want):
+        np.testing.assert_allclose(g, w, rtol=1e-6)
+    # defer_bytes caps the records a queue holds: an 8-row update keeps 608 bytes,
+    # a 5-row one 380 -> [8] [8] [8] [5 | 8] [8]
+    got, launches = run(True, defer_bytes=600)
+    assert launches == [[1] * 4] * 6
     for g, w in zip(got, want):
         np.testing.assert_allclose(g, w, rtol=1e-6)
 

@@ -1,0 +1,12 @@
+# Bench A/B: CU partition for the overlapped inversion x launch schedule.
+set -o pipefail
+mkdir -p gpurun_out
+summ() { python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; b=d['breakdown']; print(sys.argv[1], '%.3e'%d['value'], 'ms/step %.3f'%d['ms_per_step'], 'tiles %.3f inv %.3f'%(b['factor_tiles_ms_per_step'], b['invert_ms_per_step']), 'frac %.3f'%r['frac'], 'launches', r['launches'], 'serial %.3e'%(d['serial_images_per_s'] or 0))" $1; }
+for rep in 1 2; do
+for P in 0 16 32; do
+for LF in 1 16; do
+  timeout -k 10 200 python bench.py --no-cpu-baseline --no-e2e --no-serial --launch-first $LF --partition $P > gpurun_out/p${P}_lf$LF.log 2>&1 || exit 1
+  summ gpurun_out/p${P}_lf$LF.log
+done
+done
+done

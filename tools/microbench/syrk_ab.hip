@@ -1,0 +1,91 @@
+// A/B + ablation microbenchmark of the grouped SYRK tiles launch at the MLP bench's
+// job set (A1 4096k x 784 + ones, G1 x 128, A2 x 128 + ones, G2 x 10) as multi-batch
+// jobs of nb batches of 4096 rows (the queued launches of a KFAC pass: 1, 2, 4, 8).
+// Prints the tiles-launch time per variant (median of 3 x 20 launches), its TF/s on
+// the algorithmic 650,402 flop/img, and the A1-only job.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o syrk_ab syrk_ab.hip
+#include "../../bnn_kfac_amd/csrc/factor.hip"
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+namespace kfac { void prof_begin(int, hipStream_t) {} void prof_end(int, hipStream_t) {} }
+using namespace kfac;
+
+typedef void (*TilesK)(FactorArgs);
+
+static float time_k(TilesK k, const FactorArgs& a, int tasks, int reps = 20) {
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+  std::vector<float> t;
+  for (int r = 0; r < 3; ++r) {
+    hipLaunchKernelGGL(k, dim3(tasks), dim3(NTHREADS), 0, 0, a);
+    (void)hipEventRecord(e0, 0);
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(k, dim3(tasks), dim3(NTHREADS), 0, 0, a);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms; (void)hipEventElapsedTime(&ms, e0, e1);
+    t.push_back(1000.f * ms / reps);
+  }
+  std::sort(t.begin(), t.end());
+  return t[1];
+}
+
+int main(int argc, char** argv) {
+  const int B = 4096;
+  const int dims[4][2] = {{784, 1}, {128, 0}, {128, 1}, {10, 0}};  // cols, ones
+  const int maxnb = 15;
+  std::vector<float*> xs(4), Fs(4);
+  std::vector<std::vector<const float*>> bases(4);
+  for (int i = 0; i < 4; ++i) {
+    const int c = dims[i][0], n = c + dims[i][1];
+    std::vector<float> h((size_t)B * maxnb * c);
+    for (size_t e = 0; e < h.size(); ++e) h[e] = (float)((e * 2654435761u) % 1000) / 1000.f;
+    (void)hipMalloc(&xs[i], h.size() * 4);
+    (void)hipMemcpy(xs[i], h.data(), h.size() * 4, hipMemcpyHostToDevice);
+    (void)hipMalloc(&Fs[i], (size_t)n * n * 4);
+    for (int b = 0; b < maxnb; ++b) bases[i].push_back(xs[i] + (size_t)b * B * c);
+  }
+  void* ws = nullptr;
+  size_t wsb = 0;
+  const int nbs[] = {1, 8, 15};
+  for (int nb : nbs) {
+    for (int only_a1 = 0; only_a1 < 2; ++only_a1) {
+      std::vector<kfac_factor_job> jobs;
+      for (int i = 0; i < (only_a1 ? 1 : 4); ++i) {
+        kfac_factor_job j{};
+        j.x.ptr = xs[i]; j.x.layout = KFAC_ROWMAJOR; j.x.rows = B; j.x.cols = dims[i][0];
+        j.x.ld = dims[i][0]; j.x.has_ones = dims[i][1];
+        j.alpha = 1.f / B; j.beta = 0.f; j.F = Fs[i]; j.ldF = dims[i][0] + dims[i][1];
+        if (nb > 1) { j.seg_ptrs = bases[i].data(); j.nseg = nb; }
+        jobs.push_back(j);
+      }
+      const double flops = (only_a1 ? 785.0 * 786 : 650402.0) * B * nb;
+      for (int macro = 0; macro < 2; ++macro) {
+        g_syrk_macro = macro;
+        const size_t need = kfac_factor_workspace_bytes(jobs.data(), (int)jobs.size());
+        if (need > wsb) { if (ws) (void)hipFree(ws); (void)hipMalloc(&ws, need); wsb = need; }
+        GroupLaunch g;
+        if (prepare_group(jobs.data(), (int)jobs.size(), (char*)ws, wsb, g) != KFAC_OK) { printf("prep failed\n"); return 1; }
+        struct V { const char* name; TilesK k; };
+        std::vector<V> vs;
+        if (macro) {
+          vs = {{"macro", kfac_factor_tiles_macro_t<0>}, {"macro noDMA", kfac_factor_tiles_macro_t<4>},
+                {"macro regops", kfac_factor_tiles_macro_t<16>}, {"macro noDMA+regops", kfac_factor_tiles_macro_t<20>},
+                {"macro noloop", kfac_factor_tiles_macro_t<64>}};
+        } else {
+          vs = {{"t64", kfac_factor_tiles_t<32, 2, 2 | 256>}, {"t64 noDMA", kfac_factor_tiles_t<32, 2, 2 | 256 | 4>},
+                {"t64 regops", kfac_factor_tiles_t<32, 2, 2 | 256 | 16>},
+                {"t64 noDMA+regops", kfac_factor_tiles_t<32, 2, 2 | 256 | 20>},
+                {"t64 noloop", kfac_factor_tiles_t<32, 2, 2 | 256 | 64>}};
+        }
+        for (auto& v : vs) {
+          const float us = time_k(v.k, g.args, g.tasks);
+          printf("nb %d %-4s tasks %4d | %-20s %8.2f us  %6.1f TF\n", nb, only_a1 ? "A1" : "MLP", g.tasks, v.name,
+                 us, flops / us / 1e6);
+        }
+      }
+    }
+  }
+  return 0;
+}
