@@ -11,7 +11,6 @@
 //   2. kfac_factor_reduce: per tile, sum the slabs in split order, apply
 //      F = beta*F + alpha*sum, write the tile and its mirror (LDS transpose),
 //      so F stays exactly symmetric.
-#include <cmath>
 #include <utility>
 #include <vector>
 
@@ -35,7 +34,6 @@ struct FactorJobDev {
   int n, t, splits;  // factor edge, tiles per edge, K-splits
   int task_begin;    // first global task of this job
   int glds;          // row-major, 16-byte-aligned rows: LDS-DMA kernel
-  int macro;         // glds job on 128x128 macro tiles (one 64-tile per wave; t >= 2)
   int tile_begin;    // first global tile of this job (reduce launch)
   int accum;         // deferred reduction: `slab` is the caller's accumulator
   float sbeta;       // accumulator update: slab = sbeta*slab + alpha*partial
@@ -432,226 +430,6 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, const fl
   put_partial(J, acc[0], [&](int v) { return &out[acc_row(v, lane) * TILE + (lane & 31)]; });
 }
 
-// ---------------------------------------------------------------------------
-// 128x128 macro tiles (row-major, 16-byte-aligned operands, factors of more than
-// one 64-tile).  A workgroup's 4 waves each own ONE 64x64 tile of the factor's
-// lower triangle -- (2TI + w/2, 2TJ + w%2) of macro tile (TI, TJ) -- as 2x2 blocks
-// of v_mfma_f32_32x32x2f32 with 4 independent accumulators, so each 32-row stage
-// is 64 MFMAs per wave (4x the 64-tile path's 16) between two barriers, and each
-// LDS operand read feeds 2 MFMAs.  The stage's A and B panels (32 rows x 128
-// columns each; one panel on a diagonal macro tile) arrive by LDS-DMA into a 2-slot
-// ring: 64 KB per workgroup, 2 workgroups per CU (128 KB, leaving room for one
-// 32-tile inversion workgroup beside them).  Partials go to the 64-tile slab /
-// accumulator layout of the other paths (the reduce is shared).  Waves whose tile
-// is above the diagonal or past the factor's edge, and blocks of a wave's tile
-// that are, do no MFMA work.
-// Active 32x32 blocks of wave w's 64-tile in macro tile (TI, TJ) of an n x n factor
-// with t 64-tiles per edge (bit 2a+b = block (a, b)): inside the factor, in the lower
-// triangle.  0 when the wave's tile is above the diagonal or past the edge.
-__host__ __device__ inline int macro_wave_mask(int n, int t, int TI, int TJ, int w) {
-  const int ti = 2 * TI + (w >> 1), tj = 2 * TJ + (w & 1);
-  if (ti >= t || tj > ti) return 0;
-  int m = 0;
-  for (int a = 0; a < 2; ++a)
-    for (int b = 0; b < 2; ++b)
-      if (ti * TILE + a * 32 < n && tj * TILE + b * 32 < n && !(ti == tj && a < b)) m |= 1 << (2 * a + b);
-  return m;
-}
-
-template <int GBK>
-struct GldsPanel128 {
-  static constexpr int CPR = 32;                 // 16-byte chunks per 128-column row
-  static constexpr int NCH = GBK * CPR / NTHREADS;  // chunks per thread per panel (4)
-  int64_t ld, kend;
-  int ch[NCH];
-  int col[NCH];
-  bool real[NCH];
-  float4 fill[NCH];
-  __device__ __forceinline__ void init(const OpDev& op, int col0, int w, int lane, int64_t k_end) {
-    ld = op.ld; kend = k_end;
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      ch[i] = (w * NCH + i) * 64 + lane;
-      col[i] = col0 + (ch[i] & (CPR - 1)) * 4;
-      real[i] = col[i] < op.cols;
-      float f[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) f[q] = (col[i] + q == op.ones) ? 1.f : 0.f;
-      fill[i] = make_float4(f[0], f[1], f[2], f[3]);
-    }
-  }
-  __device__ __forceinline__ void issue(const float* base, int64_t k, float* slot, int w) const {
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int64_t row = k + (ch[i] / CPR);
-      const int64_t r = row < kend ? row : kend - 1;
-      const float* src = base + r * ld + (real[i] ? col[i] : 0);
-      __builtin_amdgcn_global_load_lds(src, slot + (w * NCH + i) * 256, 16, 0, 0);
-    }
-  }
-  __device__ __forceinline__ void fixup(int64_t k, float* slot) const {
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const bool okrow = k + (ch[i] / CPR) < kend;
-      if (!real[i] || !okrow) {
-        typedef float f4v __attribute__((ext_vector_type(4)));
-        const f4v v = okrow ? f4v{fill[i].x, fill[i].y, fill[i].z, fill[i].w} : f4v{0.f, 0.f, 0.f, 0.f};
-        const uint32_t addr = (uint32_t)(uintptr_t)(slot + ch[i] * 4);
-        asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
-      }
-    }
-  }
-};
-
-// The stage loop of a macro task for one set of active blocks (MASK bit 2a+b =
-// block (a, b) of the wave's 64-tile), so the MFMA stream has no guards: the
-// stage's operands (2 A + 2 B floats per k-step) are read into registers first,
-// then the MFMAs run back to back on independent accumulators.
-template <int GBK, int MASK, int MODE>
-__device__ __forceinline__ void macro_stages(const FactorJobDev& J, const float* const* segs, int64_t s0,
-                                             int ns, int TI, int TJ, bool same, bool mine, int wi, int wj,
-                                             float* lds, floatx16 (&acc)[2][2]) {
-  constexpr int MT = 2 * TILE;
-  constexpr int GSLOT = 2 * GBK * MT;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t rows = J.x.rows;
-  GldsPanel128<GBK> pa, pb;
-  pa.init(J.x, TI * MT, wave, lane, rows);
-  pb.init(J.x, TJ * MT, wave, lane, rows);
-  StageCursor ic, fc;
-  ic.init(J, s0);
-  fc = ic;
-  const float* ibase = seg_base(J, segs, ic.seg);
-  auto issue = [&](int sl) {
-    float* slot = lds + (sl & 1) * GSLOT;
-    if (!(MODE & 4)) {  // (MODE & 4: ablation without the panel loads)
-      pa.issue(ibase, ic.k, slot, wave);
-      if (!same) pb.issue(ibase, ic.k, slot + GBK * MT, wave);
-    }
-    const int seg = ic.seg;
-    ic.next(rows);
-    if (ic.seg != seg && sl + 1 < ns) ibase = seg_base(J, segs, ic.seg);
-  };
-  issue(0);
-  const int h = lane >> 5, rr = lane & 31;
-  for (int st = 0; st < ns; ++st) {
-    vm_wait(0);  // slot st landed (slot st + 1 is issued after the barrier below)
-    float* slot = lds + (st & 1) * GSLOT;
-    pa.fixup(fc.k, slot);
-    if (!same) pb.fixup(fc.k, slot + GBK * MT);
-    fc.next(rows);
-    stage_barrier();  // slot st visible to all waves; everyone is done with slot st-1
-    if (st + 1 < ns) issue(st + 1);
-    if (MASK != 0 && mine) {
-      const float* A = slot + h * MT + wi * TILE + rr;
-      const float* B = slot + (same ? 0 : GBK * MT) + h * MT + wj * TILE + rr;
-      // operands of k-step s2 + 1 are read while the MFMAs of k-step s2 issue
-      float ca0 = 0.f, ca1 = 0.f, cb0 = 0.f, cb1 = 0.f;
-      auto rd = [&](int s2, float& x0, float& x1, float& y0, float& y1) {
-        if (MODE & 16) {  // (ablation: register operands, no LDS reads)
-          x0 = x1 = (float)(lane + s2);
-          y0 = y1 = (float)(lane - s2);
-          return;
-        }
-        if (MASK & 3) x0 = A[2 * s2 * MT];
-        if (MASK & 12) x1 = A[2 * s2 * MT + 32];
-        if (MASK & 5) y0 = B[2 * s2 * MT];
-        if (MASK & 10) y1 = B[2 * s2 * MT + 32];
-      };
-      rd(0, ca0, ca1, cb0, cb1);
-#pragma unroll
-      for (int s2 = 0; s2 < GBK / 2; ++s2) {
-        float na0 = 0.f, na1 = 0.f, nb0 = 0.f, nb1 = 0.f;
-        if (s2 + 1 < GBK / 2) rd(s2 + 1, na0, na1, nb0, nb1);
-        if (MASK & 1) acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0, cb0, acc[0][0], 0, 0, 0);
-        if (MASK & 2) acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0, cb1, acc[0][1], 0, 0, 0);
-        if (MASK & 4) acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca1, cb0, acc[1][0], 0, 0, 0);
-        if (MASK & 8) acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca1, cb1, acc[1][1], 0, 0, 0);
-        ca0 = na0; ca1 = na1; cb0 = nb0; cb1 = nb1;
-      }
-    }
-  }
-}
-
-template <int GBK, int MODE = 0>
-__device__ __forceinline__ void factor_task_macro(const FactorJobDev& J, const float* const* segs,
-                                                  int local, float* lds, int split_major) {
-  const int mt = (J.t + 1) / 2;  // macro tiles per edge
-  const int nmacro = mt * (mt + 1) / 2;
-  const int split = split_major ? local / nmacro : local % J.splits;
-  const int macro = split_major ? local - split * nmacro : local / J.splits;
-  int TI, TJ;
-  tri_decode(macro, TI, TJ);
-  const int64_t s0 = (int64_t)split * J.chunk;
-  const int64_t s1 = min(J.nst, s0 + J.chunk);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wi = wave >> 1, wj = wave & 1;
-  const int ti = 2 * TI + wi, tj = 2 * TJ + wj;  // this wave's 64-tile
-  const bool same = TI == TJ;
-  const bool mine = ti < J.t && tj <= ti;
-  // (wave-uniform, through readfirstlane: scalar dispatch below)
-  const int actm = __builtin_amdgcn_readfirstlane(macro_wave_mask(J.n, J.t, TI, TJ, wave));
-  floatx16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.f;
-  const int ns = s1 > s0 ? (int)(s1 - s0) : 0;
-  if (ns > 0 && !(MODE & 64)) {
-    // every wave joins the DMA and the barriers; the mask only selects its MFMAs
-#define KFAC_MACRO_STAGES(M) \
-  macro_stages<GBK, M, MODE>(J, segs, s0, ns, TI, TJ, same, mine, wi, wj, lds, acc)
-    switch (actm) {
-      case 0xF: KFAC_MACRO_STAGES(0xF); break;
-      case 0xD: KFAC_MACRO_STAGES(0xD); break;
-      case 0x5: KFAC_MACRO_STAGES(0x5); break;
-      case 0x3: KFAC_MACRO_STAGES(0x3); break;
-      case 0x1: KFAC_MACRO_STAGES(0x1); break;
-      case 0x0: KFAC_MACRO_STAGES(0x0); break;
-      default:  // (no other pattern arises: padding only cuts the last block row / column)
-        KFAC_MACRO_STAGES(0xF); break;
-    }
-#undef KFAC_MACRO_STAGES
-  }
-  if (!mine) return;
-  float* tilep = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.splits + split) * TILE * TILE;
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      if (!((actm >> (2 * a + b)) & 1)) continue;
-      float* out = tilep + a * 32 * TILE + b * 32;
-      put_partial(J, acc[a][b], [&](int v) { return &out[acc_row(v, lane) * TILE + (lane & 31)]; });
-    }
-}
-
-// The macro-tile launch: 2 workgroups per CU; the group's other row-major jobs
-// (single 64-tiles, narrow factors, unaligned operands) take their usual task
-// functions inside it.
-template <int MODE>
-__global__ __launch_bounds__(NTHREADS, 2) void kfac_factor_tiles_macro_t(FactorArgs args) {
-  __shared__ __attribute__((aligned(16))) float lds[2 * 2 * BK * 2 * TILE];
-  if (args.stagger)
-    for (int i = 0; i < args.stagger * (int)(blockIdx.x >> 8); ++i) __builtin_amdgcn_s_sleep(8);
-  const int task = xcd_task(blockIdx.x, gridDim.x);
-  int j = 0;
-  while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
-  const FactorJobDev& J = args.job[j];
-  const int local = task - J.task_begin;
-  const float* const* segs = args.segs;
-  if (J.macro)
-    factor_task_macro<BK, MODE>(J, segs, local, lds, args.split_major);
-  else if (J.glds)
-    factor_task_glds<BK, 2, 1, 2, 1>(J, segs, local, lds, args.split_major);
-  else if (J.n <= 32)
-    factor_task_narrow_direct(J, segs, local, lds);
-  else
-    factor_task<KFAC_ROWMAJOR>(J, segs, local, lds);
-}
-
-#define kfac_factor_tiles_macro kfac_factor_tiles_macro_t<0>
 
 // One launch per grouped update.  The row-major family (FAMILY = KFAC_ROWMAJOR)
 // takes the LDS-DMA path when a job's operand allows it, else the register-staged
@@ -1100,40 +878,18 @@ static bool job_glds(const kfac_factor_job& jb) {
          (jb.x.ld % 4) == 0 && (reinterpret_cast<uintptr_t>(jb.x.ptr) % 16) == 0;
 }
 
-// 128x128 macro tiles (kfac_factor_tiles_macro) for LDS-DMA jobs of more than one
-// 64-tile; KFAC_SYRK_MACRO=0 keeps the 64-tile launch (A/B switch).
-// KFAC_SYRK_MACRO=1: 128x128 macro tiles (kfac_factor_tiles_macro) for every LDS-DMA
-// job of more than one 64-tile; 2: only for factors larger than MACRO_MIN_N; 0
-// (default): the 64-tile launch everywhere -- measured faster on the MLP (the macro
-// launch's ragged edge tiles leave half of its 2-per-CU workgroup slots idle: 274
-// vs 239 us for an 8-batch A1 update) and not faster on the wide MLP (3.16 vs 2.66
-// ms per launch), tools/microbench/syrk_ab.hip.
-static int g_syrk_macro = -1;  // -1: from the environment; microbenchmarks set it
-constexpr int MACRO_MIN_N = 1536;
-
-static bool job_macro(const kfac_factor_job& jb) {
-  if (g_syrk_macro < 0) {
-    const char* e = getenv("KFAC_SYRK_MACRO");
-    g_syrk_macro = e ? atoi(e) : 0;
-  }
-  if (g_syrk_macro == 0 || !job_glds(jb) || factor_n(jb) <= TILE) return false;
-  return g_syrk_macro == 1 || factor_n(jb) > MACRO_MIN_N;
-}
-
 static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
                       int64_t slots = 0) {
-  bool any_macro = false;
-  for (int i = 0; i < njobs; ++i) any_macro |= job_macro(jobs[i]);
-  // resident workgroups per CU: 4 (32 KB of LDS each), 2 on the macro-tile launch (64 KB)
-  if (slots <= 0) slots = (any_macro ? 2 : 4) * (int64_t)(g_cu_budget > 0 ? g_cu_budget : 256);
+  // resident workgroups per CU: 4 (32 KB of LDS each)
+  if (slots <= 0) slots = 4 * (int64_t)(g_cu_budget > 0 ? g_cu_budget : 256);
   constexpr int64_t MIN_CHUNK = 8, OVERHEAD = 4;  // stages; ~per-task fixed cost in stages
   int64_t max_steps = 1;
   for (int i = 0; i < njobs; ++i) max_steps = std::max(max_steps, job_stages(jobs[i]));
   int64_t units[MAXJ];
   for (int i = 0; i < njobs; ++i) {
-    const int64_t t = cdiv(factor_n(jobs[i]), TILE), m = (t + 1) / 2;
+    const int64_t t = cdiv(factor_n(jobs[i]), TILE);
     ConvGeom cg;
-    units[i] = conv_geom(jobs[i], cg) ? cg.units : job_macro(jobs[i]) ? m * (m + 1) / 2 : t * (t + 1) / 2;
+    units[i] = conv_geom(jobs[i], cg) ? cg.units : t * (t + 1) / 2;
   }
   // workgroups of job i at `splits` K-splits
   auto job_tasks = [&](int i, int64_t splits) { return units[i] * splits; };
@@ -1224,7 +980,6 @@ static void launch_reduce(FactorArgs& r, int tiles, hipStream_t stream) {
 struct GroupLaunch {
   FactorArgs args, red;
   int tasks, rtiles;
-  bool any_macro;
 };
 
 static int prepare_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t ws_bytes,
@@ -1242,15 +997,12 @@ static int prepare_group(const kfac_factor_job* jobs, int njobs, char* ws, size_
     args.split_major = e ? atoi(e) : 1;
   }
   int tasks = 0, rtiles = 0, nsegs = 0;
-  bool any_macro = false;
   size_t off = 0;
   for (int i = 0; i < njobs; ++i) {
     const kfac_factor_job& jb = jobs[i];
     FactorJobDev& d = args.job[i];
     fill_dev(d, jb);
     d.glds = job_glds(jb);
-    d.macro = job_macro(jb);
-    any_macro |= d.macro != 0;
     d.splits = plans[i].splits;
     d.chunk = plans[i].chunk;
     if (d.nseg > 1) {  // kfac_factor_update keeps a launch within KSEG batch bases
@@ -1275,7 +1027,6 @@ static int prepare_group(const kfac_factor_job* jobs, int njobs, char* ws, size_
   }
   g.tasks = tasks;
   g.rtiles = rtiles;
-  g.any_macro = any_macro;
   return off > ws_bytes ? KFAC_EWORKSPACE : KFAC_OK;
 }
 
@@ -1287,7 +1038,6 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
   FactorArgs& args = g.args;
   FactorArgs& red = g.red;
   const int tasks = g.tasks, rtiles = g.rtiles;
-  const bool any_macro = g.any_macro;
   if (tasks == 0) return KFAC_OK;
   {
     ProfScope ps(KFAC_PROF_FACTOR_TILES, stream);
@@ -1312,9 +1062,7 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
         {
           bool all_glds = true;
           for (int i = 0; i < njobs; ++i) all_glds &= args.job[i].glds != 0 || args.job[i].n <= 32;
-          if (any_macro)
-            hipLaunchKernelGGL(kfac_factor_tiles_macro, dim3(tasks), dim3(NTHREADS), 0, stream, args);
-          else if (all_glds)
+          if (all_glds)
             hipLaunchKernelGGL(kfac_factor_tiles_glds, dim3(tasks), dim3(NTHREADS), 0, stream, args);
           else
             hipLaunchKernelGGL(kfac_factor_tiles, dim3(tasks), dim3(NTHREADS), 0, stream, args);

@@ -1,4 +1,4 @@
-// A/B + ablation microbenchmark of the grouped SYRK tiles launch at the MLP bench's
+// Ablation microbenchmark of the grouped SYRK tiles launch at the MLP bench's
 // job set (A1 4096k x 784 + ones, G1 x 128, A2 x 128 + ones, G2 x 10) as multi-batch
 // jobs of nb batches of 4096 rows (the queued launches of a KFAC pass: 1, 2, 4, 8).
 // Prints the tiles-launch time per variant (median of 3 x 20 launches), its TF/s on
@@ -48,7 +48,10 @@ int main(int argc, char** argv) {
   }
   void* ws = nullptr;
   size_t wsb = 0;
-  const int nbs[] = {1, 8, 15};
+  std::vector<int> nbs = {1, 8, 15};
+  int only = -1;  // argv: [nb] [t64-variant index]: one configuration (for PMC passes)
+  if (argc > 1) nbs = {atoi(argv[1])};
+  if (argc > 2) only = atoi(argv[2]);
   for (int nb : nbs) {
     for (int only_a1 = 0; only_a1 < 2; ++only_a1) {
       std::vector<kfac_factor_job> jobs;
@@ -61,25 +64,21 @@ int main(int argc, char** argv) {
         jobs.push_back(j);
       }
       const double flops = (only_a1 ? 785.0 * 786 : 650402.0) * B * nb;
-      for (int macro = 0; macro < 2; ++macro) {
-        g_syrk_macro = macro;
+      {
         const size_t need = kfac_factor_workspace_bytes(jobs.data(), (int)jobs.size());
         if (need > wsb) { if (ws) (void)hipFree(ws); (void)hipMalloc(&ws, need); wsb = need; }
         GroupLaunch g;
         if (prepare_group(jobs.data(), (int)jobs.size(), (char*)ws, wsb, g) != KFAC_OK) { printf("prep failed\n"); return 1; }
         struct V { const char* name; TilesK k; };
-        std::vector<V> vs;
-        if (macro) {
-          vs = {{"macro", kfac_factor_tiles_macro_t<0>}, {"macro noDMA", kfac_factor_tiles_macro_t<4>},
-                {"macro regops", kfac_factor_tiles_macro_t<16>}, {"macro noDMA+regops", kfac_factor_tiles_macro_t<20>},
-                {"macro noloop", kfac_factor_tiles_macro_t<64>}};
-        } else {
-          vs = {{"t64", kfac_factor_tiles_t<32, 2, 2 | 256>}, {"t64 noDMA", kfac_factor_tiles_t<32, 2, 2 | 256 | 4>},
-                {"t64 regops", kfac_factor_tiles_t<32, 2, 2 | 256 | 16>},
-                {"t64 noDMA+regops", kfac_factor_tiles_t<32, 2, 2 | 256 | 20>},
-                {"t64 noloop", kfac_factor_tiles_t<32, 2, 2 | 256 | 64>}};
-        }
+        std::vector<V> vs = {{"t64", kfac_factor_tiles_t<32, 2, 2 | 256>},
+                             {"t64 noDMA", kfac_factor_tiles_t<32, 2, 2 | 256 | 4>},
+                             {"t64 regops", kfac_factor_tiles_t<32, 2, 2 | 256 | 16>},
+                             {"t64 noDMA+regops", kfac_factor_tiles_t<32, 2, 2 | 256 | 20>},
+                             {"t64 noloop", kfac_factor_tiles_t<32, 2, 2 | 256 | 64>}};
+        if (only >= 0 && only_a1) continue;
+        int vi = -1;
         for (auto& v : vs) {
+          if (only >= 0 && ++vi != only) continue;
           const float us = time_k(v.k, g.args, g.tasks);
           printf("nb %d %-4s tasks %4d | %-20s %8.2f us  %6.1f TF\n", nb, only_a1 ? "A1" : "MLP", g.tasks, v.name,
                  us, flops / us / 1e6);
