@@ -244,10 +244,15 @@ def main(argv=None):
     ap.add_argument("--no-serial", action="store_true")
     ap.add_argument("--launch-first", type=int, default=None,
                     help="queued updates in a pass's first SYRK launch (KFAC.launch_first)")
+    ap.add_argument("--sync-invert", action="store_true",
+                    help="KFAC.async_invert = False (phase 1 of each inversion issued by the caller)")
     ap.add_argument("--launch-idle", action="store_true",
                     help="KFAC.launch_policy = 'idle' (launch when the stream drains)")
     ap.add_argument("--partition", type=int, default=0,
                     help="CUs reserved for the overlapped inversion (KFAC.partition_cus; 0 = none)")
+    ap.add_argument("--single-buffer", action="store_true",
+                    help="KFAC.double_buffer = False (the data stream waits for each "
+                         "inversion to have read its factors)")
     argv = sys.argv[1:] if argv is None else argv
     args = ap.parse_args(argv)
 
@@ -293,6 +298,10 @@ def main(argv=None):
         kfac.launch_first = args.launch_first
     if args.launch_idle:
         kfac.launch_policy = "idle"
+    if args.sync_invert:
+        kfac.async_invert = False
+    if args.single_buffer:
+        kfac.double_buffer = False
     recs = synthetic_records(specs, images, device, seed=1234 + rank)
     starts = list(range(0, images, batch))
     comm = {"ms": 0.0, "n": 0, "timing": False}
@@ -340,6 +349,7 @@ def main(argv=None):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_pass()
+    t_issue = time.perf_counter() - t0  # host time to queue the K steps (diagnostic)
     # inside the timed region: join the inversion worker and read every pending
     # pivot verdict (a singular factor raises here, as the reference's would)
     kfac.inv_state
@@ -390,6 +400,7 @@ def main(argv=None):
                  "factor_reduce_ms_per_step": red_ms / args.steps,
                  "invert_ms_per_step": inv_ms / args.steps,
                  "allreduce_ms_per_step": allreduce_ms,
+                 "host_issue_ms_per_step": 1e3 * t_issue / args.steps,
                  "updates_per_step": len(starts)}
 
     serial = None

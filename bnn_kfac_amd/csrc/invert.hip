@@ -28,7 +28,10 @@
 // (one wave eliminates each 16x16 diagonal block, MFMA for the rest).
 #include <math.h>
 
+#include <string.h>
+
 #include <algorithm>
+#include <mutex>
 
 #include "kfac_common.h"
 

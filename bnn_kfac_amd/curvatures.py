@@ -176,6 +176,14 @@ class KFAC(Curvature):
                     raise NotImplementedError
         self._packed = None      # flat fp32 device buffer holding every factor
         self._packed_views = {}  # layer -> (A view, G view)
+        # Two packed buffers, alternating per data pass (reset()): an overlapped
+        # inversion reads pass k's factors while pass k+1 accumulates into the other
+        # buffer, so the caller's stream never waits for an inversion to have read its
+        # inputs; the buffer's next writer (the flush of pass k+2) waits for that
+        # inversion's inputs-read event instead (long complete by then).
+        self.double_buffer = True
+        self._alt_packed, self._alt_views = None, {}
+        self._buf_read = {}      # packed buffer data_ptr -> inputs-read event of its inversion
         self._layer_list = list(self.record)
         # Deferred execution (flush() completes it; every `state` read flushes):
         # * queued updates: update() resolves each batch's factor jobs and keeps the
@@ -244,10 +252,26 @@ class KFAC(Curvature):
         self._acc_flush = self._acc_map = None
         self._state = dict()
         self.inv_state = dict()
+        if self.double_buffer and self._packed is not None:
+            self._packed, self._packed_views, self._alt_packed, self._alt_views = (
+                self._alt_packed, self._alt_views, self._packed, self._packed_views)
+            if self._packed is None:
+                self._packed_views = {}
+
+    def _await_readers(self, stream=None):
+        """Order the caller's (or the given) stream after the inversion that read the
+        current packed buffer, before that buffer is written or handed out."""
+        buf = self._packed
+        if buf is None or not self._buf_read:
+            return
+        ev = self._buf_read.pop(buf.data_ptr(), None)
+        if ev is not None:
+            (stream or torch.cuda.current_stream(buf.device)).wait_event(ev)
 
     def flush(self):
         """Launch queued updates, then reduce the pending accumulators into the
-        factors (async; one reduce launch)."""
+        factors (async; one reduce launch).  Afterwards the caller's stream is ordered
+        after any inversion still reading the factors (`state` hands them out)."""
         if getattr(self, "_queue", None):
             self._launch_queue()
         self._launch_at = getattr(self, "launch_first", 1)
@@ -255,12 +279,18 @@ class KFAC(Curvature):
         if jobs:
             self._acc_flush = self._acc_map = None
             self._end_cycle(jobs)
+        if getattr(self, "_buf_read", None):
+            self._await_readers()
 
     def _end_cycle(self, jobs):
         """Reduce the cycle's accumulators into the factors; the caller's stream then
         waits for the cycle's stream (every later reader of `state` is behind it)."""
         device = self._acc_device
-        self._on_cycle_stream(device, lambda: N.factor_flush(jobs, device))
+
+        def reduce():
+            self._await_readers()  # (on the stream the reduce is issued on)
+            N.factor_flush(jobs, device)
+        self._on_cycle_stream(device, reduce)
         ds, self._cycle_stream = self._cycle_stream, None
         if ds is not None:
             torch.cuda.current_stream(device).wait_stream(ds)
@@ -393,6 +423,7 @@ class KFAC(Curvature):
         total = sum(nA * nA + nG * nG for _, nA, nG in sizes)
         if self._packed is not None and self._packed.numel() == total and self._packed.device == device:
             return
+        self._await_readers()  # the buffer dropped here may still be read by an inversion
         buf = torch.empty(total, dtype=torch.float32, device=device)
         views, off = {}, 0
         for layer, nA, nG in sizes:
@@ -448,6 +479,7 @@ class KFAC(Curvature):
             jobs.append(N.factor_job(opG, G, self._alpha(opG), beta))
             keep.extend(kept)
         if not self.defer_reduce:
+            self._await_readers()
             N.factor_update(jobs, device)
             return
         self._remember(prepared, jobs, device)
@@ -677,7 +709,7 @@ class KFAC(Curvature):
                     pair.append(out)
                 outs.append((layer, tuple(pair)))
             if read is not None and self.async_invert:
-                return self._invert_async(device, main, side, part_side, jobs, outs, read)
+                return self._invert_async(device, main, side, part_side, jobs, outs, read, entries)
             info = N.invert(jobs, device, inputs_read=read)
             # The pivot verdict travels back with a non-blocking copy into pinned
             # memory; it is settled (event wait) at the next read of `inv_state` or the
@@ -700,13 +732,13 @@ class KFAC(Curvature):
                 done = torch.cuda.Event()
                 done.record(cs)
         if read is not None:
-            main.wait_event(read)
+            self._release(main, read, entries)
         for layer, pair in outs:
             self._inv_state[layer] = pair
         self._inv_pending = (done, host, [layer for layer, _ in outs], self._inv_state,
                              [t for _, pair in outs for t in pair], side is not main, part_side, None)
 
-    def _invert_async(self, device, main, side, part_side, jobs, outs, read):
+    def _invert_async(self, device, main, side, part_side, jobs, outs, read, entries):
         """invert() with overlap_invert: phase 0 (the launches that read F) here, the
         caller's stream released behind it, phase 1 + the verdict readback from the
         worker thread (every later use of the pending inversion joins it first)."""
@@ -714,7 +746,7 @@ class KFAC(Curvature):
         arr, ws, info = N.invert_prepare(jobs, device, sh)
         N.invert_phase(arr, ws, info, 0, sh)
         read.record(side)
-        main.wait_event(read)
+        self._release(main, read, entries)
         pool = self._info_pool
         while pool and pool[-1].numel() != info.numel():
             pool.pop()
@@ -742,6 +774,18 @@ class KFAC(Curvature):
             self._inv_state[layer] = pair
         self._inv_pending = (done, host, [layer for layer, _ in outs], self._inv_state,
                              [t for _, pair in outs for t in pair], True, part_side, fut)
+
+    def _release(self, main, read, entries):
+        """Let the caller's stream go past an inversion: straight away when the factors
+        it reads are one of the double-buffered packed buffers (the buffer's next
+        writer waits for `read` instead, see _await_readers), else behind `read`."""
+        buf = self._packed
+        if self.double_buffer and buf is not None:
+            base = buf.untyped_storage().data_ptr()
+            if all(F_.untyped_storage().data_ptr() == base for _, v in entries for F_ in v):
+                self._buf_read[buf.data_ptr()] = read
+                return
+        main.wait_event(read)
 
     @staticmethod
     def _joined(pending):

@@ -66,6 +66,7 @@ class DistributedKFAC(KFAC):
     def __init__(self, model: Union[Module, Sequential], layer_types: Union[List[str], str] = None,
                  process_group=None, shard_inversion="auto"):
         super().__init__(model, layer_types)
+        self.double_buffer = False  # reset() rotates the local / reduced buffers itself
         self.group = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0

@@ -101,8 +101,21 @@ def test_update_host_logic_with_double(monkeypatch):
     np.testing.assert_allclose(A0.numpy(), ref.state["l0"][0], rtol=1e-5)
     np.testing.assert_allclose(G0.numpy(), ref.state["l0"][1], rtol=1e-5)
     np.testing.assert_allclose(kfac.state[net[2]][0].numpy(), ref.state["l1"][0], rtol=1e-5)
+    # reset() alternates two packed buffers (an overlapped inversion reads one while
+    # the next pass accumulates into the other); the second is allocated lazily
+    first = kfac._packed
     kfac.reset()
-    assert kfac.state == {} and kfac._packed is not None
+    assert kfac.state == {} and kfac._packed is None and kfac._alt_packed is first
+    kfac.record[net[0]] = [torch.from_numpy(a1), torch.from_numpy(g1)]
+    kfac.record[net[2]] = [torch.from_numpy(a2), torch.from_numpy(g2)]
+    kfac.update(B)
+    second = kfac._packed
+    assert second is not None and second.data_ptr() != first.data_ptr()
+    kfac.reset()
+    assert kfac._packed is first and kfac._alt_packed is second
+    kfac.double_buffer = False
+    kfac.reset()
+    assert kfac._packed is first
 
 
 def test_deferred_reduce_host_logic(monkeypatch):

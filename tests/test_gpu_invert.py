@@ -147,11 +147,14 @@ def test_invert_identity_property_wide(hip_device):
     assert np.abs(E - np.eye(n)).max() < 1e-3
 
 
-def test_overlapped_inversion_matches_serial(hip_device):
+@pytest.mark.parametrize("reset", [True, False])
+def test_overlapped_inversion_matches_serial(hip_device, reset):
     """invert() runs on the side stream and the next pass is queued right behind it
     (the bench's pattern: nothing read in between, so pass k+1's SYRK overlaps
-    inversion k and its flush overwrites the factors inversion k read).  Every
-    pass's L factors equal the serial path's bit for bit."""
+    inversion k).  With reset() the passes alternate two packed buffers and pass
+    k+2's flush overwrites the buffer inversion k read; without it every flush adds
+    into the buffer the previous inversion is reading.  Every pass's L factors equal
+    the serial path's bit for bit."""
     from bnn_kfac_amd.curvatures import KFAC
     torch.manual_seed(0)
     net = nn.Sequential(nn.Linear(784, 128), nn.ReLU(), nn.Linear(128, 10)).to(hip_device)
@@ -168,7 +171,8 @@ def test_overlapped_inversion_matches_serial(hip_device):
         kfac.partition_cus = 0  # one stream layout: same SYRK splits as the serial path
         kept = []
         for batches in passes:
-            kfac.reset()
+            if reset:
+                kfac.reset()
             for a1, g1, a2, g2 in batches:
                 kfac.record[net[0]] = [a1, g1]
                 kfac.record[net[2]] = [a2, g2]
