@@ -11,8 +11,11 @@
 // off(A)^2 <= (1e-15)^2 * ||A||_F^2 (checked once per sweep).  Output sorted
 // ascending by a parallel rank pass.
 #include <math.h>
+#include <stdlib.h>
 
 #include <algorithm>
+#include <vector>
+#include <stdio.h>
 
 #include "kfac_common.h"
 
@@ -158,216 +161,527 @@ __global__ __launch_bounds__(NTHREADS) void eig_jacobi_lds(EigArgs args) {
 // ---------------------------------------------------------------------------
 // n > 128: Householder tridiagonalisation + Sturm bisection (eigenvalues).
 //
-// eig_tridiag: ONE persistent launch per factor.  G workgroups, row i owned by
-// workgroup i % G (slot i / G), the owned rows kept in LDS for the whole
-// reduction (fp64, symmetrised).  Step k (reflector for column k):
-//   phase A (row-local): p_i = tau * sum_j A[i][j] u_j, partial c = sum p_i u_i
-//   -- grid barrier --
-//   phase B (row-local): w = p - (tau c / 2) u ;  A[i][j] -= u_i w_j + w_i u_j,
-//            then the next column A[i][k+1] (and its partial norm) is published
-//   -- grid barrier --
-// Every workgroup derives the reflector scalars redundantly from the published
-// partials, so the only cross-workgroup data are u / p / two partial vectors.
-// Grid barriers: agent-scope release (one lane, after the workgroup barrier) on
-// an arrival counter, agent-scope acquire poll, bounded spins; a timeout sets
-// `abort` and every workgroup leaves at its next barrier (the launch always
-// drains; the host reports the timeout as info = -1).
+// eig_tridiag: ONE persistent launch per factor, ONE grid-wide exchange per
+// reflector.  G workgroups, row i owned by workgroup i % G (slot i / G), the owned
+// rows kept in LDS (fp64, symmetrised) when they fit, else in a global slab only
+// their owner touches.  Every workgroup holds the full vectors x (the column the
+// next reflector comes from), u and w in LDS.  Step k:
+//   1. (every workgroup, redundantly, same bits) reflector u, tau from x;
+//   2. (own rows i > k) ONE pass over the row: apply the previous step's rank-2
+//      update lazily (A[i][j] -= u'_i w'_j + w'_i u'_j), read a_i = A_k[i][k+1] and
+//      p_i = tau * A_k[i][k+1:] . u;
+//   3. exchange: publish (p_i, a_i) and c_wg = sum p_i u_i; read everyone's;
+//   4. (every workgroup) w = p - (tau c / 2) u and the next column
+//      x'_i = a_i - u_i w_{k+1} - w_i u_{k+1}, its sigma for step k+1.
+// (The row pass of step k+1 applies (u, w) to the rows.)
+//
+// The exchange is the data-tagged granule form of the MI355X in-launch hand-off
+// (no flag, no fence): every published 32-bit half of a fp64 value travels as ONE
+// aligned 8-byte {tag = epoch, bits} granule written by one `sc1` store; a reader
+// re-reads its granules with `sc1` loads until every tag equals the step's epoch.
+// Granules are double-buffered by step parity (a workgroup publishes step k+1 only
+// after it has seen every workgroup's step-k granules, i.e. after every workgroup
+// finished reading step k-1's).  All granules are zeroed before the launch (epochs
+// start at 1).  Waits are bounded (1 s): a timeout sets `abort`, and every
+// workgroup leaves at its next wait (the launch drains; info = -1).
+
+typedef __attribute__((address_space(1))) unsigned long long eg_u64;
+typedef __attribute__((address_space(1))) unsigned eg_unsigned;
+typedef unsigned long long gran_t;
+__device__ __forceinline__ void st_gran(gran_t* g, unsigned tag, unsigned bits) {
+  __hip_atomic_store((eg_u64*)g, ((gran_t)tag << 32) | bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_gran_d(gran_t* g, unsigned tag, double v) {  // 2 granules
+  const gran_t b = (gran_t)__double_as_longlong(v);
+  st_gran(g, tag, (unsigned)b);
+  st_gran(g + 1, tag, (unsigned)(b >> 32));
+}
+__device__ __forceinline__ gran_t ld_gran(const gran_t* g) {
+  return __hip_atomic_load((eg_u64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Two granules (one fp64 value) by ONE 16-byte `sc1` buffer load (aux 16 = sc1);
+// each 8-byte half is checked by its own tag.
+typedef unsigned gv4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void ld_gran2(__amdgpu_buffer_rsrc_t rs, int off_bytes, gran_t& g0, gran_t& g1) {
+  const gv4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, off_bytes, 0, 16);
+  g0 = ((gran_t)v.y << 32) | v.x;
+  g1 = ((gran_t)v.w << 32) | v.z;
+}
+__device__ __forceinline__ double gran_d(gran_t lo, gran_t hi) {
+  return __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
+}
+__device__ __forceinline__ bool gran_ok(gran_t g, unsigned tag) { return (unsigned)(g >> 32) == tag; }
+__device__ __forceinline__ unsigned ldu_ag(const unsigned* p) {
+  return __hip_atomic_load((eg_unsigned*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stu_ag(unsigned* p, unsigned v) {
+  __hip_atomic_store((eg_unsigned*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One wave's spin bookkeeping (wave-uniform): false once the launch is aborted or
+// this wave's deadline has passed (then it sets the abort word).
+struct Spin {
+  uint64_t deadline = 0;
+  unsigned spins = 0;
+  // the abort word and the clock are read every 8th spin only (a spin is one sweep
+  // of the granules; the first deadline is set at the first check)
+  __device__ bool again(unsigned* abort) {
+    if ((++spins & 7u) == 0u) {
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (deadline == 0) deadline = now + 100000000ull;  // 1 s at 100 MHz
+      if (__builtin_amdgcn_readfirstlane(ldu_ag(abort)) != 0u) return false;
+      if (now > deadline) {
+        stu_ag(abort, 1u);
+        return false;
+      }
+    }
+    __builtin_amdgcn_s_sleep(1);
+    return true;
+  }
+};
 
 struct TriArgs {
   const float* F;
   int64_t ldF;
   int n, G, R;         // rows per workgroup R = ceil(n / G)
   double* rows_g;      // G x R x n owned rows when they do not fit LDS (else null)
-  double* x;           // 2 x n: published columns (double-buffered by step parity)
-  double* p;           // n
-  double* cpart;       // G
-  double* spart;       // G
+  gran_t* pub;         // 2 (step parity) x n x 4 granules {p lo, p hi, a lo, a hi}
+  unsigned* abort;     // timeout flag
   double* d;           // n: diagonal of T
   double* e;           // n: off-diagonal of T (e[k] = T[k+1][k])
-  unsigned* bar;       // arrival counter (zeroed before the launch)
-  unsigned* abort;     // timeout flag (zeroed before the launch)
   double* U;           // n x n: row k = reflector u_k (entries k+1..n-1), or null
   double* tau;         // n: reflector scales (0: no reflection), or null
+  uint64_t* stamps;    // debug (KFAC_EIG_PROF): per step 5 s_memrealtime stamps of workgroup 0
 };
 
-__device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned* abort, unsigned target) {
-  __syncthreads();  // every wave's stores issued and waited (vmcnt 0) before the release
-  __shared__ int bail;
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    int ok = 1;
-    for (unsigned spins = 0;; ++spins) {
-      if (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
-      if (__hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
-          spins > (1u << 22)) {
-        __hip_atomic_store(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    bail = !ok;
-  }
-  __syncthreads();
-  return !bail;
+// Wave sum in registers (no LDS crossbar): quad_perm xor 1 / xor 2 and row_ror 4 / 8
+// DPP within each 16-lane row, then permlane16_swap / permlane32_swap across rows.
+// Lane 0's value is the one used (lanes may associate differently); the same tree
+// runs in every workgroup -> bit-identical scalars everywhere.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xf, 0xf, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double wave_sum(double v) {
+  v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_d<0x124>(v);  // row_ror:4
+  v += dpp_d<0x128>(v);  // row_ror:8
+  unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const auto pl = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+  const auto ph = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  v = __builtin_bit_cast(double, ((unsigned long long)ph[0] << 32) | pl[0]) +
+      __builtin_bit_cast(double, ((unsigned long long)ph[1] << 32) | pl[1]);
+  b = __builtin_bit_cast(unsigned long long, v);
+  const auto ql = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+  const auto qh = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  return __builtin_bit_cast(double, ((unsigned long long)qh[0] << 32) | ql[0]) +
+         __builtin_bit_cast(double, ((unsigned long long)qh[1] << 32) | ql[1]);
 }
 
-// deterministic: same tree in every workgroup -> bit-identical scalars everywhere
+// fixed pairwise tree over W per-wave values (the same in every workgroup)
+template <int W, class F>
+__device__ __forceinline__ double wsum(F f) {
+  if constexpr (W == 4) {
+    return (f(0) + f(1)) + (f(2) + f(3));
+  } else {
+    double t[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) t[w] = f(w);
+#pragma unroll
+    for (int h = W / 2; h > 0; h >>= 1)
+#pragma unroll
+      for (int w = 0; w < h; ++w) t[w] += t[w + h];
+    return t[0];
+  }
+}
+template <int W>
+__device__ __forceinline__ double block_sum_w(double v, double* red) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return wsum<W>([&](int w) { return red[w]; });
+}
+template <int W>
+__device__ __forceinline__ double block_sum1_w(double v, double* red) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return wsum<W>([&](int w) { return red[w]; });
+}
+
+// one barrier: the caller guarantees a barrier between the reads of `red` here and
+// the next write of the same slot
+__device__ __forceinline__ double block_sum1(double v, double* red) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 __device__ __forceinline__ double block_sum(double v, double* red) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  v = wave_sum(v);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-template <bool LDS_ROWS>
+constexpr int TRI_CH = 8;  // columns per thread per sweep (4 granules each)
+
+template <bool LDS_ROWS, int RB>
 __global__ __launch_bounds__(NTHREADS) void eig_tridiag(TriArgs a) {
-  extern __shared__ double lds[];  // [u n][w n][rows R x n if LDS_ROWS]
-  __shared__ double red[NTHREADS / 64];
+  constexpr int TB = NTHREADS, W = TB / 64, CH = TRI_CH;
+  extern __shared__ double lds[];  // [v0 n][v1 n][w n][rows R x n if LDS_ROWS]
+  __shared__ double red[TB / 64];
+  __shared__ int fail_s;
   const int n = a.n, G = a.G, wg = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  double* uS = lds;
-  double* wS = lds + n;
-  double* rows = LDS_ROWS ? lds + 2 * n : a.rows_g + (size_t)wg * a.R * n;
-  unsigned epoch = 0;
+  // x / u share a slot (u is built in place from x); the previous u is the other
+  // slot; w is rewritten after each row pass (the previous w is dead by then)
+  double* vs[2] = {lds, lds + n};
+  double* wS = lds + 2 * n;
+  double* rows = LDS_ROWS ? lds + 3 * n : a.rows_g + (size_t)wg * a.R * n;
   auto row_of = [&](int slot) { return slot * G + wg; };
   auto A = [&](int slot) { return rows + (size_t)slot * n; };
+  if (tid == 0) fail_s = 0;
+  for (int j = tid; j < n; j += TB) {  // the "previous step" of step 0: u = w = 0
+    vs[1][j] = 0.0;
+    wS[j] = 0.0;
+  }
 
-  // load + symmetrise the owned rows; publish column 0 (step 0's x)
+  // load + symmetrise the owned rows; publish column 0 (epoch 1, parity 1: step 0
+  // publishes into parity 0)
   for (int s = 0; s < a.R; ++s) {
     const int i = row_of(s);
     if (i >= n) break;
-    for (int j = tid; j < n; j += NTHREADS)
+    for (int j = tid; j < n; j += TB)
       A(s)[j] = 0.5 * ((double)a.F[(int64_t)i * a.ldF + j] + (double)a.F[(int64_t)j * a.ldF + i]);
   }
   __syncthreads();
-  {
-    double sig = 0.0;
-    for (int s = tid; s < a.R; s += NTHREADS) {
-      const int i = row_of(s);
-      if (i >= n) continue;
-      const double v = A(s)[0];
-      if (i >= 1) a.x[i] = v;
-      if (i >= 2) sig += v * v;
-      if (i == 0) a.d[0] = v;
-    }
-    sig = block_sum(sig, red);
-    if (tid == 0) a.spart[wg] = sig;
+  gran_t* pub1 = a.pub + (size_t)4 * n;
+  for (int s = tid; s < a.R; s += TB) {
+    const int i = row_of(s);
+    if (i < n) st_gran_d(pub1 + 4 * (size_t)i + 2, 1u, A(s)[0]);
   }
-  if (!grid_sync(a.bar, a.abort, (++epoch) * G)) return;
+  double* x = vs[0];
+  double sig = 0.0;
+  {
+    Spin sp;
+    for (int j0 = 0; j0 < n; j0 += CH * TB) {
+      gran_t g[CH][2];
+      bool ok;
+      for (;;) {
+        ok = true;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+          const int j = j0 + c * TB + tid;
+          if (j < n) {
+            g[c][0] = ld_gran(pub1 + 4 * (size_t)j + 2);
+            g[c][1] = ld_gran(pub1 + 4 * (size_t)j + 3);
+            ok = ok && gran_ok(g[c][0], 1u) && gran_ok(g[c][1], 1u);
+          }
+        }
+        if (__builtin_amdgcn_readfirstlane(__all(ok))) break;
+        if (!sp.again(a.abort)) break;
+      }
+      if (!__builtin_amdgcn_readfirstlane(__all(ok))) {
+        if (lane == 0) fail_s = 1;
+        break;
+      }
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const int j = j0 + c * TB + tid;
+        if (j < n) {
+          const double v = gran_d(g[c][0], g[c][1]);
+          x[j] = v;
+          if (j >= 2) sig += v * v;
+        }
+      }
+    }
+  }
+  double sigma = block_sum_w<W>(sig, red);  // (its barriers also publish x and fail_s)
+  if (fail_s) return;
+  if (wg == 0 && tid == 0) a.d[0] = x[0];
+  double* up = vs[1];  // previous step's u (unused at k = 0)
 
+  auto stamp = [&](int k, int at) {
+    if (a.stamps && wg == 0 && tid == 0) {
+      a.stamps[(size_t)k * 5 + at] = __builtin_amdgcn_s_memrealtime();
+      if (at == 0) a.stamps[(size_t)8192 * 5 + k] = __builtin_amdgcn_s_memtime();
+    }
+  };
+  __shared__ double rp[2][TB / 64][RB];  // per-wave partial dots of a row batch (batch parity)
+  __shared__ double p1_s;
+  __shared__ double red2[TB / 64];           // block_sum slot of the sigma reduction
+  const __amdgpu_buffer_rsrc_t pub_rs =
+      __builtin_amdgcn_make_buffer_rsrc(a.pub, 0, (int)(2 * 4 * (size_t)n * sizeof(gran_t)), 0x00020000);
   for (int k = 0; k + 2 < n; ++k) {
-    const double* xk = a.x + (size_t)(k & 1) * n;
-    // reflector scalars (every workgroup, redundantly, same order -> same bits)
-    const double sigma = block_sum(tid < G ? a.spart[tid] : 0.0, red);
-    const double alpha = xk[k + 1];
+    const unsigned tag = (unsigned)k + 2u;
+    stamp(k, 0);
+    gran_t* pub = a.pub + (size_t)(k & 1) * 4 * n;
+    // 1. reflector (every workgroup, redundantly, same order -> same bits)
+    const double alpha = x[k + 1];
     double tau = 0.0, u0 = 0.0, beta = alpha;
     if (sigma > 0.0) {
       beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
       u0 = alpha - beta;
       tau = 2.0 / (u0 * u0 + sigma);
     }
-    if (wg == 0 && tid == 0) a.e[k] = beta;
-    const bool keep_u = a.U && wg == k % G;  // reflectors kept for the eigenvector back-transform
-    if (a.U && wg == 0 && tid == 0) a.tau[k] = tau;
-    for (int j = k + 1 + tid; j < n; j += NTHREADS) {
-      const double uj = j == k + 1 ? u0 : xk[j];
-      uS[j] = uj;
-      if (keep_u) a.U[(size_t)k * n + j] = uj;
+    // u_j = x_j for j >= k+2 (the x slot is read as u); u_{k+1} = u0 stays in a
+    // register (no barrier: nothing reads u[k+1] from LDS, and the next step's row
+    // pass reads its previous u only at rows / columns >= k+2)
+    const double* u = x;
+    auto u_at = [&](int j) { return j == k + 1 ? u0 : u[j]; };
+    if (wg == 0 && tid == 0) {
+      a.e[k] = beta;
+      if (a.U) a.tau[k] = tau;
     }
-    __syncthreads();
+    if (a.U && wg == k % G)  // reflectors kept for the eigenvector back-transform
+      for (int j = k + 1 + tid; j < n; j += TB) a.U[(size_t)k * n + j] = u_at(j);
+    stamp(k, 1);
 
-    // phase A: p_i = tau * A[i][k+1:] . u, one wave per owned row
-    double cp = 0.0;
-    for (int s = wave; s < a.R; s += NTHREADS / 64) {
-      const int i = row_of(s);
-      if (i >= n) break;
-      if (i <= k) continue;
-      double acc = 0.0;
-      for (int j = k + 1 + lane; j < n; j += 64) acc += A(s)[j] * uS[j];
-      for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-      acc *= tau;
-      if (lane == 0) {
-        a.p[i] = acc;
-        cp += acc * uS[i];
+    // 2. row pass, thread per column, RB owned rows at a time: the lazy rank-2
+    //    update of step k-1, then a_i (column k+1) and p_i = tau A_k[i][k+1:] . u
+    //    (per-thread partials, wave shuffles, one barrier per batch)
+    const int s_lo = k + 1 > wg ? (k + 1 - wg + G - 1) / G : 0;  // first slot with row > k
+    for (int s0 = s_lo, bp = 0; s0 < a.R; s0 += RB, bp ^= 1) {
+      // a batch past the last slot repeats the last slot (read-before-write per column,
+      // so the repeat writes the same values); slots whose row is >= n hold unused
+      // rows.  Their results are never published.  (up / wS start zero: the k = 0
+      // "update" subtracts nothing.)
+      double acc[RB], upi[RB], wsi[RB];
+      double* Ar[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const int sl = min(s0 + r, a.R - 1);
+        const int i = min(row_of(sl), n - 1);  // (an unused slot's row: any valid index)
+        Ar[r] = A(sl);
+        upi[r] = up[i];
+        wsi[r] = wS[i];
+        acc[r] = 0.0;
+      }
+      for (int j = k + 1 + tid; j < n; j += TB) {
+        const double uj = u_at(j), upj = up[j], wj = wS[j];
+        double v[RB];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) v[r] = Ar[r][j];  // every load first
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          v[r] -= upi[r] * wj + wsi[r] * upj;
+          Ar[r][j] = v[r];
+          acc[r] += v[r] * uj;
+        }
+      }
+      if constexpr (W == 1) {
+        // one wave: lane 0 holds the sums and wrote column k+1 itself; no barrier
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const double v = wave_sum(acc[r]);
+          if (lane == 0 && s0 + r < a.R && row_of(s0 + r) < n) {
+            const int i = row_of(s0 + r);
+            st_gran_d(pub + 4 * (size_t)i, tag, tau * v);
+            st_gran_d(pub + 4 * (size_t)i + 2, tag, Ar[r][k + 1]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const double v = wave_sum(acc[r]);
+          if (lane == 0) rp[bp][wave][r] = v;
+        }
+        __syncthreads();  // (the next batch writes the other parity: one barrier per batch)
+        if (tid < RB && s0 + tid < a.R && row_of(s0 + tid) < n) {
+          const int i = row_of(s0 + tid);
+          const double pi = tau * (wsum<W>([&](int w) { return rp[bp][w][tid]; }));
+          st_gran_d(pub + 4 * (size_t)i, tag, pi);
+          st_gran_d(pub + 4 * (size_t)i + 2, tag, A(s0 + tid)[k + 1]);
+        }
       }
     }
-    cp = block_sum(cp, red);
-    if (tid == 0) a.cpart[wg] = cp;
-    if (!grid_sync(a.bar, a.abort, (++epoch) * G)) return;
+    stamp(k, 2);
 
-    // phase B: rank-2 update of the owned trailing rows, publish column k+1
-    const double K = 0.5 * tau * block_sum(tid < G ? a.cpart[tid] : 0.0, red);
-    for (int j = k + 1 + tid; j < n; j += NTHREADS) wS[j] = a.p[j] - K * uS[j];
-    __syncthreads();
-    for (int s = 0; s < a.R; ++s) {
-      const int i = row_of(s);
-      if (i >= n) break;
-      if (i <= k) continue;
-      const double ui = uS[i], wi = wS[i];
-      for (int j = k + 1 + tid; j < n; j += NTHREADS) A(s)[j] -= ui * wS[j] + wi * uS[j];
+    // 3. exchange: every (p_j, a_j), j > k; c = sum p_j u_j from the gathered p
+    //    (same tree in every workgroup), then w_j, x'_j.  Up to CH columns per
+    //    thread per sweep; the last sweep's granules stay in registers.
+    gran_t g[CH][4];
+    double cs = 0.0;
+    const int nch = (n - (k + 1) + CH * TB - 1) / (CH * TB);
+    {
+      Spin sp;
+      for (int ch = 0; ch < nch; ++ch) {
+        const int j0 = k + 1 + ch * CH * TB;
+        bool ok;
+        for (;;) {
+          ok = true;
+#pragma unroll
+          for (int cc = 0; cc < CH; ++cc) {
+            const int j = j0 + cc * TB + tid;
+            if (j < n) {
+              const int off = (int)(((size_t)(k & 1) * 4 * n + 4 * (size_t)j) * sizeof(gran_t));
+              ld_gran2(pub_rs, off, g[cc][0], g[cc][1]);
+              ld_gran2(pub_rs, off + 16, g[cc][2], g[cc][3]);
+#pragma unroll
+              for (int h = 0; h < 4; ++h) ok = ok && gran_ok(g[cc][h], tag);
+            }
+          }
+          if (__builtin_amdgcn_readfirstlane(__all(ok))) break;
+          if (!sp.again(a.abort)) break;
+        }
+        if (!__builtin_amdgcn_readfirstlane(__all(ok))) {
+          if (lane == 0) fail_s = 1;
+          break;
+        }
+#pragma unroll
+        for (int cc = 0; cc < CH; ++cc) {
+          const int j = j0 + cc * TB + tid;
+          if (j < n) {
+            const double pj = gran_d(g[cc][0], g[cc][1]);
+            cs += pj * u_at(j);
+            if (j == k + 1) p1_s = pj;
+          }
+        }
+      }
     }
-    __syncthreads();
-    double* xn = a.x + (size_t)((k + 1) & 1) * n;
-    double sig = 0.0;
-    for (int s = tid; s < a.R; s += NTHREADS) {
-      const int i = row_of(s);
-      if (i >= n) continue;
-      const double v = A(s)[k + 1];
-      if (i == k + 1) a.d[k + 1] = v;
-      if (i >= k + 2) xn[i] = v;
-      if (i >= k + 3) sig += v * v;
+    const double c = block_sum1_w<W>(cs, red);  // (its barrier also publishes p1_s and fail_s)
+    stamp(k, 3);
+    if (fail_s) return;
+    const double K = 0.5 * tau * c;
+    const double u1 = u0;
+    const double w1 = p1_s - K * u1;
+    double* xn = up;  // the previous u's slot is dead now
+    sig = 0.0;
+    for (int q = 0; q < nch; ++q) {
+      // the last chunk first (its granules are still in registers), then the others
+      // reloaded (arrived and checked in the sweep)
+      const int ch = q == 0 ? nch - 1 : q - 1;
+      const int j0 = k + 1 + ch * CH * TB;
+      if (q > 0) {
+#pragma unroll
+        for (int cc = 0; cc < CH; ++cc) {
+          const int j = j0 + cc * TB + tid;
+          if (j < n) {
+            const int off = (int)(((size_t)(k & 1) * 4 * n + 4 * (size_t)j) * sizeof(gran_t));
+            ld_gran2(pub_rs, off, g[cc][0], g[cc][1]);
+            ld_gran2(pub_rs, off + 16, g[cc][2], g[cc][3]);
+          }
+        }
+      }
+#pragma unroll
+      for (int cc = 0; cc < CH; ++cc) {
+        const int j = j0 + cc * TB + tid;
+        if (j < n) {
+          const double uj = u_at(j);
+          const double wj = gran_d(g[cc][0], g[cc][1]) - K * uj;
+          const double xj = gran_d(g[cc][2], g[cc][3]) - (uj * w1 + wj * u1);
+          wS[j] = wj;
+          xn[j] = xj;
+          if (j >= k + 3) sig += xj * xj;
+        }
+      }
     }
-    sig = block_sum(sig, red);
-    if (tid == 0) a.spart[wg] = sig;
-    if (!grid_sync(a.bar, a.abort, (++epoch) * G)) return;
+    // every wave is past its row pass (the c barrier), so wS / xn could be rewritten
+    // above; the sigma barrier publishes them (and separates this step's reads of
+    // `red` / `red2` from the next step's writes of the other slot)
+    sigma = block_sum1_w<W>(sig, red2);
+    stamp(k, 4);
+    if (wg == 0 && tid == 0) a.d[k + 1] = xn[k + 1];
+    up = x;
+    x = xn;
   }
-  // tail: T[n-1][n-1] and T[n-1][n-2] from their owner
-  if (n >= 2 && tid == 0) {
+  // tail: T[n-1][n-2] is the last column's sub-diagonal entry; T[n-1][n-1] is row
+  // n-1's diagonal with the last step's update applied (by its owner)
+  if (wg == 0 && tid == 0) a.e[n - 2] = x[n - 1];
+  if (tid == 0) {
     for (int s = 0; s < a.R; ++s) {
-      if (row_of(s) == n - 1) {
-        a.d[n - 1] = A(s)[n - 1];
-        a.e[n - 2] = A(s)[n - 2];
-      }
+      if (row_of(s) == n - 1) a.d[n - 1] = A(s)[n - 1] - 2.0 * up[n - 1] * wS[n - 1];
     }
   }
 }
 
-// Eigenvalues of the symmetric tridiagonal (d, e) by Sturm-count bisection, one
-// thread per eigenvalue index (k-th smallest -> ascending order for free).
+// Eigenvalues of the symmetric tridiagonal (d, e) by Sturm-count multisection:
+// ONE wave per eigenvalue index k (the k-th smallest -> ascending order for free).
+// Each round the 64 lanes count the eigenvalues below 64 interior points of the
+// current interval [lo, hi] (LDL^T inertia, one lane per point) and the interval
+// shrinks to the 1/65 slice where the count crosses k: ~9 rounds of one O(n)
+// recurrence reach fp64 resolution, where one-point bisection needs ~55 (the
+// recurrence is a chain of dependent fp64 divisions, so rounds, not flops, are the
+// cost).  d and e^2 are staged in LDS once per workgroup.
 __global__ __launch_bounds__(NTHREADS) void eig_bisect(const double* d, const double* e, int n,
                                                        double* evals, const unsigned* abort, int* info) {
-  const int k = blockIdx.x * NTHREADS + threadIdx.x;
-  if (k == 0 && info) *info = *abort ? -1 : 0;
-  if (k >= n) return;
+  extern __shared__ double sh[];  // [d n][e^2 n]
+  double* dS = sh;
+  double* e2S = sh + n;
+  __shared__ double red[2][NTHREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (blockIdx.x == 0 && tid == 0 && info) *info = *abort ? -1 : 0;
   double lo = 0.0, hi = 0.0, emax2 = 0.0;
-  for (int i = 0; i < n; ++i) {
-    const double r = (i > 0 ? fabs(e[i - 1]) : 0.0) + (i + 1 < n ? fabs(e[i]) : 0.0);
-    lo = i ? fmin(lo, d[i] - r) : d[i] - r;
-    hi = i ? fmax(hi, d[i] + r) : d[i] + r;
-    if (i + 1 < n) emax2 = fmax(emax2, e[i] * e[i]);
+  for (int i = tid; i < n; i += NTHREADS) {
+    const double di = d[i], ei = i + 1 < n ? e[i] : 0.0;
+    dS[i] = di;
+    e2S[i] = ei * ei;
+    const double r = (i > 0 ? fabs(e[i - 1]) : 0.0) + fabs(ei);
+    lo = i == tid ? di - r : fmin(lo, di - r);
+    hi = i == tid ? di + r : fmax(hi, di + r);
+    emax2 = fmax(emax2, ei * ei);
   }
+  // Gershgorin bounds over the whole matrix (lanes without rows contribute nothing)
+  const bool any = tid < n;
+  double glo = any ? lo : INFINITY, ghi = any ? hi : -INFINITY;
+  for (int o = 32; o > 0; o >>= 1) {
+    glo = fmin(glo, __shfl_xor(glo, o));
+    ghi = fmax(ghi, __shfl_xor(ghi, o));
+    emax2 = fmax(emax2, __shfl_xor(emax2, o));
+  }
+  if (lane == 0) {
+    red[0][tid >> 6] = glo;
+    red[1][tid >> 6] = ghi;
+  }
+  __shared__ double em_s[NTHREADS / 64];
+  if (lane == 0) em_s[tid >> 6] = emax2;
+  __syncthreads();
+  lo = fmin(fmin(red[0][0], red[0][1]), fmin(red[0][2], red[0][3]));
+  hi = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
+  emax2 = fmax(fmax(em_s[0], em_s[1]), fmax(em_s[2], em_s[3]));
+  const int k = blockIdx.x * (NTHREADS / 64) + (tid >> 6);
+  if (k >= n) return;  // (wave-uniform; no barrier follows)
   const double pivmin = 1e-290 * fmax(1.0, emax2);
   const double span = fmax(fabs(lo), fabs(hi));
   lo -= 2.2e-16 * span + pivmin;
   hi += 2.2e-16 * span + pivmin;
-  for (int it = 0; it < 200; ++it) {
-    const double mid = 0.5 * (lo + hi);
-    if (hi - lo <= 2.0 * 2.2e-16 * fmax(fabs(lo), fabs(hi)) + pivmin || mid == lo || mid == hi) break;
+  for (int it = 0; it < 40; ++it) {
+    if (hi - lo <= 2.0 * 2.2e-16 * fmax(fabs(lo), fabs(hi)) + pivmin) break;
+    const double step = (hi - lo) * (1.0 / 65.0);
+    const double mid = lane == 63 ? hi - step : lo + step * (double)(lane + 1);
     // count of eigenvalues < mid (LDL^T inertia)
     int cnt = 0;
-    double q = d[0] - mid;
+    double q = dS[0] - mid;
     if (fabs(q) < pivmin) q = -pivmin;
     cnt += q < 0.0;
     for (int i = 1; i < n; ++i) {
-      q = d[i] - mid - e[i - 1] * e[i - 1] / q;
+      // e^2 / q by v_rcp_f64 + two Newton steps (|q| >= pivmin, so no 0 / inf
+      // cases; the division's scaling / fixup steps are not needed): a few-ulp
+      // quotient, under which the inertia count stays backward stable
+      double r = __builtin_amdgcn_rcp(q);
+      r = fma(r, fma(-q, r, 1.0), r);
+      r = fma(r, fma(-q, r, 1.0), r);
+      q = (dS[i] - mid) - e2S[i - 1] * r;
       if (fabs(q) < pivmin) q = -pivmin;
       cnt += q < 0.0;
     }
-    if (cnt > k) hi = mid; else lo = mid;
+    const unsigned long long above = __ballot(cnt > k);  // lanes whose point is above eigenvalue k
+    const int first = above ? __builtin_ctzll(above) : 64;
+    const double nlo = first == 0 ? lo : __shfl(mid, first - 1);
+    const double nhi = first == 64 ? hi : __shfl(mid, first == 64 ? 0 : first);
+    if (nlo == lo && nhi == hi) break;  // no representable progress
+    lo = nlo;
+    hi = nhi;
   }
-  evals[k] = 0.5 * (lo + hi);
+  if (lane == 0) evals[k] = 0.5 * (lo + hi);
 }
 
 }  // namespace kfac
@@ -514,24 +828,51 @@ __global__ __launch_bounds__(NTHREADS) void eig_backtransform(const double* U, c
     for (int q = 0; q < nv; ++q) evecs[(int64_t)i * ldv + j0 + q] = (float)vs[q * n + i];
 }
 
-// n > EIG_LDS_MAX: tridiagonalisation plan (grid, rows per workgroup, row storage)
+// n > EIG_LDS_MAX: tridiagonalisation plan (grid, rows per workgroup, row storage).
+// Rows in LDS when some G <= 256 fits them: the fewest workgroups that do (the
+// exchange's cost grows with G, the row pass's shrinks; env KFAC_EIG_G overrides
+// within what fits).  Otherwise 256 workgroups with the rows in a global slab.
 struct TriPlan {
-  int G, R;
+  int G, R, RB;  // workgroups, rows per workgroup, rows per row-pass batch
   bool lds_rows;
   size_t shmem, ws;
 };
 constexpr size_t TRI_LDS_BUDGET = 150 * 1024;
 
+static int eig_g_env() {
+  const char* v = getenv("KFAC_EIG_G");
+  return v ? atoi(v) : 0;
+}
+
+// the block zeroed before every launch: abort word, then the granules
+static size_t tri_zero_bytes(int n) {
+  return 256 + align_up((size_t)2 * 4 * n * sizeof(gran_t), 256);  // pub: 2 parities x n x 4
+}
+
 static TriPlan tri_plan(int n, bool vecs) {
   TriPlan p;
-  p.G = std::min(256, std::max(1, (n + 7) / 8));
+  const size_t vec = (size_t)3 * n * sizeof(double);
+  const size_t row = (size_t)n * sizeof(double);
+  const int rmax = vec < TRI_LDS_BUDGET ? (int)((TRI_LDS_BUDGET - vec) / row) : 0;
+  const int gmin = rmax > 0 ? (n + rmax - 1) / rmax : 1 << 30;
+  p.lds_rows = gmin <= 256;
+  if (p.lds_rows) {
+    // ~8 rows per workgroup (two row-pass batches): n = 785 -> 99 workgroups.  Measured
+    // per step at 785 (tools/gpu/eig_clk.sh): G = 64 / 96 / 128 / 160 / 256 ->
+    // 5.1 / 4.8 / 4.8 / 5.2 / 5.2 us (fewer rows per workgroup shorten the row pass,
+    // more workgroups lengthen the exchange)
+    p.G = std::max(gmin, std::min(256, (n + 7) / 8));
+    const int env = eig_g_env();
+    if (env > 0) p.G = std::max(gmin, std::min(1024, env));
+  } else {
+    p.G = 256;
+  }
   p.R = (n + p.G - 1) / p.G;
-  p.lds_rows = (size_t)(2 + p.R) * n * sizeof(double) <= TRI_LDS_BUDGET;
-  p.shmem = (size_t)(p.lds_rows ? 2 + p.R : 2) * n * sizeof(double);
-  p.ws = 256                                                    // bar, abort (+pad)
-         + align_up((size_t)2 * n * sizeof(double), 256)        // x
-         + 3 * align_up((size_t)n * sizeof(double), 256)        // p, d, e
-         + 2 * align_up(256 * sizeof(double), 256)              // cpart, spart
+  const char* rb = getenv("KFAC_EIG_RB");
+  p.RB = rb && atoi(rb) == 8 ? 8 : 4;  // 4 rows per batch measured faster at every G tried
+  p.shmem = vec + (p.lds_rows ? (size_t)p.R * row : 0);
+  p.ws = tri_zero_bytes(n)                                       // abort + granules
+         + 2 * align_up((size_t)n * sizeof(double), 256)         // d, e
          + (p.lds_rows ? 0 : align_up((size_t)p.G * p.R * n * sizeof(double), 256))
          + (vecs ? 2 * align_up((size_t)n * n * sizeof(double), 256)  // U, Z
                        + 5 * align_up((size_t)n * cdiv(n, NTHREADS) * NTHREADS * sizeof(double), 256)
@@ -546,15 +887,11 @@ static int tridiag_eig(const kfac_eig_job& j, char* ws, int32_t* info, hipStream
   if (pl.shmem > TRI_LDS_BUDGET) return KFAC_EINVAL;
   TriArgs t{};
   t.F = j.F; t.ldF = j.ldF; t.n = j.n; t.G = pl.G; t.R = pl.R;
-  t.bar = reinterpret_cast<unsigned*>(ws);
-  t.abort = t.bar + 1;
+  t.abort = reinterpret_cast<unsigned*>(ws);
   char* q = ws + 256;
-  t.x = reinterpret_cast<double*>(q); q += align_up((size_t)2 * j.n * sizeof(double), 256);
-  t.p = reinterpret_cast<double*>(q); q += align_up((size_t)j.n * sizeof(double), 256);
+  t.pub = reinterpret_cast<gran_t*>(q); q += align_up((size_t)2 * 4 * j.n * sizeof(gran_t), 256);
   t.d = reinterpret_cast<double*>(q); q += align_up((size_t)j.n * sizeof(double), 256);
   t.e = reinterpret_cast<double*>(q); q += align_up((size_t)j.n * sizeof(double), 256);
-  t.cpart = reinterpret_cast<double*>(q); q += align_up(256 * sizeof(double), 256);
-  t.spart = reinterpret_cast<double*>(q); q += align_up(256 * sizeof(double), 256);
   t.rows_g = pl.lds_rows ? nullptr : reinterpret_cast<double*>(q);
   if (!pl.lds_rows) q += align_up((size_t)pl.G * pl.R * j.n * sizeof(double), 256);
   double *Z = nullptr, *scratch = nullptr;
@@ -568,18 +905,55 @@ static int tridiag_eig(const kfac_eig_job& j, char* ws, int32_t* info, hipStream
     // reflector rows start zero below their support (the back-transform reads u[k+1..])
     if (hipMemsetAsync(t.tau, 0, (size_t)j.n * sizeof(double), stream) != hipSuccess) return KFAC_ELAUNCH;
   }
-  if (hipMemsetAsync(ws, 0, 16, stream) != hipSuccess) return KFAC_ELAUNCH;
-  const void* fn = pl.lds_rows ? reinterpret_cast<const void*>(&eig_tridiag<true>)
-                               : reinterpret_cast<const void*>(&eig_tridiag<false>);
+  // abort word and every granule start at zero (tag 0 never matches an epoch)
+  if (hipMemsetAsync(ws, 0, tri_zero_bytes(j.n), stream) != hipSuccess) return KFAC_ELAUNCH;
+  const bool rb8 = pl.RB == 8;
+  const void* fn = pl.lds_rows ? (rb8 ? reinterpret_cast<const void*>(&eig_tridiag<true, 8>)
+                                      : reinterpret_cast<const void*>(&eig_tridiag<true, 4>))
+                               : (rb8 ? reinterpret_cast<const void*>(&eig_tridiag<false, 8>)
+                                      : reinterpret_cast<const void*>(&eig_tridiag<false, 4>));
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.shmem) != hipSuccess)
     return KFAC_ELAUNCH;
+  static uint64_t* prof = nullptr;  // debug: step-phase stamps (KFAC_EIG_PROF=1; synchronises)
+  const bool want_prof = getenv("KFAC_EIG_PROF") != nullptr;
+  if (want_prof) {
+    if (!prof && hipMalloc(&prof, (size_t)8192 * 6 * sizeof(uint64_t)) != hipSuccess) return KFAC_ELAUNCH;
+    if (j.n > 8192) return KFAC_EINVAL;
+    t.stamps = prof;
+  }
   void* kargs[] = {&t};
   // cooperative: the runtime rejects a grid that cannot be co-resident (no deadlock)
   if (hipLaunchCooperativeKernel(fn, dim3(pl.G), dim3(NTHREADS), kargs, (unsigned)pl.shmem, stream) !=
       hipSuccess)
     return KFAC_ELAUNCH;
-  hipLaunchKernelGGL(eig_bisect, dim3((j.n + NTHREADS - 1) / NTHREADS), dim3(NTHREADS), 0, stream,
-                     t.d, t.e, j.n, j.evals, t.abort, info);
+  if (want_prof) {
+    std::vector<uint64_t> h((size_t)j.n * 5), clk((size_t)j.n);
+    if (hipMemcpyAsync(h.data(), prof, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipMemcpyAsync(clk.data(), prof + (size_t)8192 * 5, clk.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                       stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+      return KFAC_ELAUNCH;
+    fprintf(stderr, "eig_tridiag shader clock %.0f MHz\n",
+            (double)(clk[(size_t)j.n - 3] - clk[0]) / (double)(h[(size_t)(j.n - 3) * 5] - h[0]) * 100.0);
+    double ph[5] = {0, 0, 0, 0, 0};
+    const int steps = j.n - 2;
+    for (int k = 0; k < steps; ++k) {
+      for (int q = 0; q < 4; ++q) ph[q] += (double)(h[(size_t)k * 5 + q + 1] - h[(size_t)k * 5 + q]);
+      if (k + 1 < steps) ph[4] += (double)(h[(size_t)(k + 1) * 5] - h[(size_t)k * 5 + 4]);
+    }
+    fprintf(stderr, "eig_tridiag n=%d G=%d R=%d: us/step reflector %.2f rowpass+publish %.2f "
+            "sweep1+c %.2f sweep2+x %.2f tail %.2f total %.2f ms\n", j.n, pl.G, pl.R,
+            ph[0] / steps / 100.0, ph[1] / steps / 100.0, ph[2] / steps / 100.0, ph[3] / steps / 100.0,
+            ph[4] / steps / 100.0, (double)(h[(size_t)(steps - 1) * 5 + 4] - h[0]) / 1e5);
+  }
+  // one wave per eigenvalue; d and e^2 in LDS (2 n doubles <= 64 KiB up to n = 4096)
+  const size_t bsh = (size_t)2 * j.n * sizeof(double);
+  if (bsh > TRI_LDS_BUDGET) return KFAC_EINVAL;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&eig_bisect),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)bsh) != hipSuccess)
+    return KFAC_ELAUNCH;
+  hipLaunchKernelGGL(eig_bisect, dim3((j.n + NTHREADS / 64 - 1) / (NTHREADS / 64)), dim3(NTHREADS), bsh,
+                     stream, t.d, t.e, j.n, j.evals, t.abort, info);
   KFAC_CHECK_LAUNCH();
   if (vecs) {
     hipLaunchKernelGGL(eig_tri_vectors, dim3((j.n + NTHREADS - 1) / NTHREADS), dim3(NTHREADS), 0,
