@@ -435,6 +435,10 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, const fl
 // takes the LDS-DMA path when a job's operand allows it, else the register-staged
 // row-major path; channel-major and im2col jobs get launches (and register budgets)
 // of their own, instantiated per layout.
+// MODE & 512 (microbenchmarks only): per-workgroup start / end s_memrealtime stamps
+__device__ unsigned long long g_syrk_stamps[2 * 16384];
+__device__ unsigned g_syrk_hw[2 * 16384];  // HW_ID, XCC_ID of the workgroup
+
 template <int GBK, int NSLOT, int MODE = 0, int SUB = 1, int FAMILY = KFAC_ROWMAJOR>
 __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs args) {
   constexpr int RING = FAMILY == KFAC_ROWMAJOR ? NSLOT * 2 * GBK * TILE : 0;
@@ -453,6 +457,22 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
   while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
   const FactorJobDev& J = args.job[j];
   const int local = task - J.task_begin;
+  if constexpr ((MODE & 512) != 0) {
+    if (threadIdx.x == 0 && blockIdx.x < 16384) {
+      g_syrk_stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+      g_syrk_hw[2 * blockIdx.x] = __builtin_amdgcn_s_getreg(4 | (31 << 11));       // HW_REG_HW_ID
+      g_syrk_hw[2 * blockIdx.x + 1] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
+    }
+  }
+  struct StampEnd {
+    __device__ ~StampEnd() {
+      if constexpr ((MODE & 512) != 0) {
+        __syncthreads();
+        if (threadIdx.x == 0 && blockIdx.x < 16384)
+          g_syrk_stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+      }
+    }
+  } stamp_end;
   if constexpr (FAMILY == KFAC_ROWMAJOR) {
     const float* const* segs = args.segs;
     if constexpr ((MODE & 256) != 0) {
@@ -899,7 +919,12 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
     return n;
   };
   int64_t best_c = std::max(MIN_CHUNK, max_steps), best_cost = -1;
-  for (int64_t r = 1; r <= 4; ++r) {
+  static const int forced_rounds = [] {
+    const char* v = getenv("KFAC_SYRK_ROUNDS");
+    return v ? atoi(v) : 0;
+  }();
+  for (int64_t r = 1; r <= 8; ++r) {
+    if (forced_rounds > 0 ? r != forced_rounds : r > 4) continue;
     int64_t lo = MIN_CHUNK, hi = std::max(MIN_CHUNK, max_steps);
     if (tasks_at(hi) > r * slots) continue;  // even one split per tile needs more rounds
     while (lo < hi) {

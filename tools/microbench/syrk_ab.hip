@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+#include <map>
 namespace kfac { void prof_begin(int, hipStream_t) {} void prof_end(int, hipStream_t) {} }
 using namespace kfac;
 
@@ -74,7 +75,8 @@ int main(int argc, char** argv) {
                              {"t64 noDMA", kfac_factor_tiles_t<32, 2, 2 | 256 | 4>},
                              {"t64 regops", kfac_factor_tiles_t<32, 2, 2 | 256 | 16>},
                              {"t64 noDMA+regops", kfac_factor_tiles_t<32, 2, 2 | 256 | 20>},
-                             {"t64 noloop", kfac_factor_tiles_t<32, 2, 2 | 256 | 64>}};
+                             {"t64 noloop", kfac_factor_tiles_t<32, 2, 2 | 256 | 64>},
+                             {"t64 stamps", kfac_factor_tiles_t<32, 2, 2 | 256 | 512>}};
         if (only >= 0 && only_a1) continue;
         int vi = -1;
         for (auto& v : vs) {
@@ -82,6 +84,70 @@ int main(int argc, char** argv) {
           const float us = time_k(v.k, g.args, g.tasks);
           printf("nb %d %-4s tasks %4d | %-20s %8.2f us  %6.1f TF\n", nb, only_a1 ? "A1" : "MLP", g.tasks, v.name,
                  us, flops / us / 1e6);
+          if (v.k == kfac_factor_tiles_t<32, 2, 2 | 256 | 512> && g.tasks <= 16384) {
+            // the last timed launch's per-workgroup stamps (100 MHz): when workgroups
+            // start / end relative to the first start, and how long each one runs
+            std::vector<unsigned long long> st(2 * 16384);
+            (void)hipDeviceSynchronize();
+            (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_syrk_stamps), st.size() * 8);
+            unsigned long long t0 = ~0ull;
+            for (int b = 0; b < g.tasks; ++b) t0 = std::min(t0, st[2 * b]);
+            std::vector<double> s0, e0, d0;
+            for (int b = 0; b < g.tasks; ++b) {
+              s0.push_back((st[2 * b] - t0) / 100.0);
+              e0.push_back((st[2 * b + 1] - t0) / 100.0);
+              d0.push_back((st[2 * b + 1] - st[2 * b]) / 100.0);
+            }
+            auto pct = [](std::vector<double> x, double q) { std::sort(x.begin(), x.end()); return x[(size_t)(q * (x.size() - 1))]; };
+            printf("    start us p0 %.1f p50 %.1f p100 %.1f | end p10 %.1f p50 %.1f p90 %.1f p100 %.1f | "
+                   "dur p0 %.1f p50 %.1f p100 %.1f\n", pct(s0, 0), pct(s0, .5), pct(s0, 1), pct(e0, .1), pct(e0, .5),
+                   pct(e0, .9), pct(e0, 1), pct(d0, 0), pct(d0, .5), pct(d0, 1));
+            if (only_a1) {
+              // A1 alone (one job, split-major): durations by tile kind, and by how many
+              // workgroups share the CU
+              std::vector<unsigned> hw(2 * 16384);
+              (void)hipMemcpyFromSymbol(hw.data(), HIP_SYMBOL(g_syrk_hw), hw.size() * 4);
+              const int T = 13, ntiles = T * (T + 1) / 2, n = g.tasks;
+              std::vector<double> full, diag, edge;
+              std::map<unsigned, std::vector<int>> cu;
+              for (int b = 0; b < n; ++b) {
+                const int x = b & 7, sl = b >> 3, per = n >> 3, rem = n & 7;
+                const int task = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + sl;
+                const int tile = task % ntiles;
+                int ti = 0;
+                while ((ti + 1) * (ti + 2) / 2 <= tile) ++ti;
+                const int tj = tile - ti * (ti + 1) / 2;
+                (ti == T - 1 ? edge : ti == tj ? diag : full).push_back(d0[b]);
+                const unsigned id = hw[2 * b], cu_key = (hw[2 * b + 1] << 16) | (((id >> 13) & 7) << 8) |
+                                                        (((id >> 12) & 1) << 4) | ((id >> 8) & 15);
+                cu[cu_key].push_back(b);
+              }
+              printf("    full %zu dur p10 %.1f p50 %.1f p90 %.1f | diag %zu p50 %.1f | edge %zu p50 %.1f\n",
+                     full.size(), pct(full, .1), pct(full, .5), pct(full, .9), diag.size(), pct(diag, .5),
+                     edge.size(), pct(edge, .5));
+              std::map<int, std::vector<double>> by_occ;
+              for (auto& kv : cu)
+                for (int b : kv.second) by_occ[(int)kv.second.size()].push_back(d0[b]);
+              std::map<int, std::vector<double>> by_xcc, by_cu_end;
+              for (auto& kv : cu)
+                for (int b : kv.second) by_xcc[(int)(kv.first >> 16)].push_back(d0[b]);
+              printf("    per XCC dur p50:");
+              for (auto& kv : by_xcc) printf(" %d:%.0f", kv.first, pct(kv.second, .5));
+              printf("\n    per CU (4 WG) mean dur, sorted p0/p25/p50/p75/p100:");
+              std::vector<double> cum;
+              for (auto& kv : cu) {
+                if (kv.second.size() != 4) continue;
+                double m = 0;
+                for (int b : kv.second) m += d0[b] / 4;
+                cum.push_back(m);
+              }
+              printf(" %.0f %.0f %.0f %.0f %.0f\n", pct(cum, 0), pct(cum, .25), pct(cum, .5), pct(cum, .75), pct(cum, 1));
+              printf("    CUs used %zu;", cu.size());
+              for (auto& kv : by_occ) printf(" %d WG/CU: %zu WGs dur p50 %.1f max %.1f;", kv.first, kv.second.size(),
+                                             pct(kv.second, .5), pct(kv.second, 1));
+              printf("\n");
+            }
+          }
         }
       }
     }
