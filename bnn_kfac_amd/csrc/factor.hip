@@ -13,6 +13,7 @@
 //      so F stays exactly symmetric.
 #include <utility>
 #include <vector>
+#include <type_traits>
 
 #include "kfac_common.h"
 
@@ -546,6 +547,15 @@ struct ConvGeom {
 template <int LAYOUT, int PMAXE, bool STRIDE1, int CB = CONV_CB>
 __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args, ConvGeom cg) {
   extern __shared__ __attribute__((aligned(16))) float cimg[];
+#ifdef KFAC_CONV_STAMPS  // microbenchmarks only: per-workgroup start / end stamps
+  if (threadIdx.x == 0 && blockIdx.x < 16384) g_syrk_stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+  struct StampEnd {
+    __device__ ~StampEnd() {
+      if (threadIdx.x == 0 && blockIdx.x < 16384)
+        g_syrk_stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+  } stamp_end;
+#endif
   const int task = xcd_task(blockIdx.x, gridDim.x);
   int jx = 0;
   while (jx + 1 < args.njobs && task >= args.task_end[jx]) ++jx;
@@ -553,7 +563,10 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args,
   const OpDev& op = J.x;
   const int local = task - J.task_begin;
   const int unit = local / J.splits, split = local - unit * J.splits;  // unit: block group
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index through readfirstlane: the block bookkeeping derived from it (same[],
+  // nmine, the row groups) is then wave-uniform (scalar branches, no exec-mask
+  // juggling around the operand reads of the MFMA chain)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int mode = cg.mode;
   const int klane = mode == 2 ? lane >> 4 : lane >> 5;
   const int64_t b0 = (int64_t)split * cg.B / J.splits, b1 = (int64_t)(split + 1) * cg.B / J.splits;
@@ -568,20 +581,22 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args,
       if (LAYOUT == KFAC_PATCH) {
         const int hw = op.H * op.W, c = e / hw, r = e - c * hw, h = r / op.W, w = r - h * op.W;
         d = c * cg.plane + (h + op.ph) * cg.Wp + (w + op.pw);
-      } else {
+      } else {  // float index of the float4's first element (planes need not be 4-aligned)
         const int L4 = (int)op.L >> 2, c = e / L4;
-        d = (c * cg.plane >> 2) + (e - c * L4);
+        d = c * cg.plane + 4 * (e - c * L4);
       }
     }
     dmap[q] = d;
   }
-  floatx4 pre[PMAXE];  // PATCH uses [0]
+  // next image in flight: PATCH stages single floats, CHANNEL float4s
+  using PreT = std::conditional_t<LAYOUT == KFAC_PATCH, float, floatx4>;
+  PreT pre[PMAXE];
   auto fetch = [&](int64_t b) {
     const float* src = op.ptr + b * op.sB;
 #pragma unroll
     for (int q = 0; q < PMAXE; ++q) {
       if (dmap[q] < 0) continue;
-      if (LAYOUT == KFAC_PATCH) pre[q][0] = src[tid + q * NTHREADS];
+      if constexpr (LAYOUT == KFAC_PATCH) pre[q] = src[tid + q * NTHREADS];
       else pre[q] = reinterpret_cast<const floatx4*>(src)[tid + q * NTHREADS];
     }
   };
@@ -589,8 +604,12 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args,
 #pragma unroll
     for (int q = 0; q < PMAXE; ++q) {
       if (dmap[q] < 0) continue;
-      if (LAYOUT == KFAC_PATCH) cimg[dmap[q]] = pre[q][0];
-      else reinterpret_cast<floatx4*>(cimg)[dmap[q]] = pre[q];
+      if constexpr (LAYOUT == KFAC_PATCH) {
+        cimg[dmap[q]] = pre[q];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cimg[dmap[q] + r] = pre[q][r];
+      }
     }
   };
 
@@ -635,16 +654,68 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args,
 
   // one row group of one block: T MFMAs, operands read two MFMAs ahead (LDS latency
   // off the accumulator chain)
-  auto row_mfmas = [&](const float* pa, const float* pb, bool sm, auto mfma) {
+  // Operands in chunks of CK steps, double-buffered: chunk c+1's LDS reads are issued
+  // before chunk c's MFMAs, so each read has CK MFMAs (>= 128 cycles) to land.  (B is
+  // read even where it equals A -- a diagonal block: one more LDS read, but no select
+  // that would make the next MFMA wait for the read.)
+  auto row_mfmas = [&](const float* pa, const float* pb, bool, auto mfma) {
+    constexpr int CK = 4;
     const int st = STRIDE1 ? 1 : cg.stride, T = cg.T, last = (T - 1) * st;
-    float a0 = pa[0], b0 = sm ? a0 : pb[0];
-    float a1 = pa[min(st, last)], b1 = sm ? a1 : pb[min(st, last)];
-    for (int t = 0; t < T; ++t) {
-      const int o = min((t + 2) * st, last);
-      const float a2 = pa[o], b2 = sm ? a2 : pb[o];
-      mfma(a0, b0);
-      a0 = a1; b0 = b1;
-      a1 = a2; b1 = b2;
+    float ca[CK], cb[CK], na[CK], nb[CK];
+#pragma unroll
+    for (int u = 0; u < CK; ++u) {
+      const int o = min(u * st, last);
+      ca[u] = pa[o];
+      cb[u] = pb[o];
+    }
+    for (int t0 = 0; t0 < T; t0 += CK) {
+#pragma unroll
+      for (int u = 0; u < CK; ++u) {
+        const int o = min((t0 + CK + u) * st, last);
+        na[u] = pa[o];
+        nb[u] = pb[o];
+      }
+#pragma unroll
+      for (int u = 0; u < CK; ++u)
+        if (t0 + u < T) mfma(ca[u], cb[u]);
+#pragma unroll
+      for (int u = 0; u < CK; ++u) {
+        ca[u] = na[u];
+        cb[u] = nb[u];
+      }
+    }
+  };
+  // two blocks (CB = 2) of one row group: operands for CK steps of both blocks per
+  // chunk, double-buffered as in row_mfmas, MFMAs alternating between the blocks
+  auto row_mfmas2 = [&](const float* pa0, const float* pb0, const float* pa1, const float* pb1) {
+    constexpr int CK = 4;
+    const int st = STRIDE1 ? 1 : cg.stride, T = cg.T, last = (T - 1) * st;
+    float ca[2][CK], cb[2][CK], na[2][CK], nb[2][CK];
+#pragma unroll
+    for (int u = 0; u < CK; ++u) {
+      const int o = min(u * st, last);
+      ca[0][u] = pa0[o]; cb[0][u] = pb0[o];
+      ca[1][u] = pa1[o]; cb[1][u] = pb1[o];
+    }
+    for (int t0 = 0; t0 < T; t0 += CK) {
+#pragma unroll
+      for (int u = 0; u < CK; ++u) {
+        const int o = min((t0 + CK + u) * st, last);
+        na[0][u] = pa0[o]; nb[0][u] = pb0[o];
+        na[1][u] = pa1[o]; nb[1][u] = pb1[o];
+      }
+#pragma unroll
+      for (int u = 0; u < CK; ++u) {
+        if (t0 + u < T) {
+          acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[0][u], cb[0][u], acc[0], 0, 0, 0);
+          acc[CB - 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[1][u], cb[1][u], acc[CB - 1], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < CK; ++u) {
+        ca[0][u] = na[0][u]; cb[0][u] = nb[0][u];
+        ca[1][u] = na[1][u]; cb[1][u] = nb[1][u];
+      }
     }
   };
   // one row group of every block of this wave (rowA / rowB: LDS offsets added to the
@@ -653,6 +724,12 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args,
     if (mode == 2) {
       row_mfmas(cimg + (zeroA ? cg.zero_base : offA[0] + rowA), cimg + offB[0] + rowB, true,
                 [&](float a, float b) { acc16 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc16, 0, 0, 0); });
+      return;
+    }
+    if (CB == 2 && nmine == 2) {
+      // both blocks in one pass, their MFMAs alternating (two independent chains)
+      row_mfmas2(cimg + (zeroA ? cg.zero_base : offA[0] + rowA), cimg + offB[0] + rowB,
+                 cimg + (zeroA ? cg.zero_base : offA[1] + rowA), cimg + offB[1] + rowB);
       return;
     }
 #pragma unroll
@@ -734,10 +811,26 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
   g.KR = g.mode == 2 ? 4 : 2;
   g.B = (int)(o.rows / o.L);
   int64_t lds;
+  // Bank-conflict-free operand reads: an MFMA's 32 lanes of one lane group read 32
+  // consecutive factor columns, column (c, ki, kj) at c*plane + ki*Wp + kj (PATCH) or
+  // c*plane (CHANNEL) plus a lane-uniform offset.  ds_read_b32 banks are
+  // (addr / 4) mod 32, so with Wp = kw and plane = kh*kw (PATCH) or plane = 1
+  // (CHANNEL) modulo 32 every lane hits the bank of its own column index.  (16x16x4
+  // CHANNEL blocks put two k-lanes in a group: their segments are 16 apart mod 32.)
+  auto pad_to = [](int64_t v, int64_t r) { return v + (((r - v) % 32) + 32) % 32; };
   if (o.layout == KFAC_PATCH) {
     if ((int64_t)o.C * o.H * o.W > CONV_SRC_MAX) return false;
     g.Wp = o.W + 2 * o.pw;
     g.plane = (o.H + 2 * o.ph) * g.Wp;
+    if (g.mode != 2) {
+      const int64_t Wp = pad_to(g.Wp, o.kw);
+      const int64_t plane = pad_to((int64_t)(o.H + 2 * o.ph) * Wp, (int64_t)o.kh * o.kw);
+      const int64_t need = o.C * plane + 2 * (int64_t)o.Ho * o.sh * Wp;
+      if (need <= CONV_LDS_MAX) {
+        g.Wp = (int)Wp;
+        g.plane = (int)plane;
+      }
+    }
     g.Ho = o.Ho;
     g.rowstep = o.sh * g.Wp;
     g.T = o.Wo;
@@ -753,9 +846,10 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
         img / 4 > CONV_SRC_MAX)
       return false;
     const int segs = g.mode ? 4 * g.KR : g.KR;  // narrow: the 4 waves' segments too
-    const int Q = (int)(cdiv(cdiv(o.L, segs), 4) * 4);
+    int Q = (int)cdiv(o.L, segs);
+    if (g.mode == 2) Q = (int)pad_to(Q, 16);
     g.rowstep = Q;
-    g.plane = segs * Q;
+    g.plane = (int)pad_to((int64_t)segs * Q, 1);
     g.T = Q;
     g.G = 1;
     g.stride = 1;
@@ -949,7 +1043,23 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
     }
     p.splits = (int)cdiv(steps, best_c);
     ConvGeom cg;
-    if (conv_geom(jobs[i], cg)) p.splits = std::min(p.splits, cg.B);  // tasks own whole images
+    if (conv_geom(jobs[i], cg)) {
+      // Tasks own whole images, the SAME number k each, and fill the resident slots
+      // once: k = the fewest images per task that keep units x ceil(B / k) tasks
+      // within the slots.  A workgroup's time is k times a per-image cost, so a mix of
+      // 2- and 3-image tasks waited on the 3-image ones, and a CU running more
+      // workgroups than another finished later (LeNet-5, batch 1024: conv2 A 68 us at
+      // 400 splits -> 53 us at k = 2 (1,024 tasks); conv1 A 34 -> 27 us at k = 1;
+      // tools/microbench/conv_ab.hip, KFAC_CONV_K overrides k)
+      int k = (int)std::max<int64_t>(1, cdiv((int64_t)cg.units * cg.B, slots));
+      static const int env_k = [] {
+        const char* v = getenv("KFAC_CONV_K");
+        return v ? atoi(v) : 0;
+      }();
+      if (env_k > 0) k = env_k;
+      k = std::min(k, cg.B);
+      p.splits = (int)cdiv(cg.B, k);
+    }
     p.chunk = cdiv(steps, (int64_t)p.splits);
     p.slab_bytes = align_up((size_t)p.tiles * p.splits * TILE * TILE * sizeof(float), 256);
     p.tasks = (int)job_tasks(i, p.splits);

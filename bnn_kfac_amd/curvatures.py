@@ -384,11 +384,15 @@ class KFAC(Curvature):
         if layer.__class__.__name__ == 'Conv2d':
             if isinstance(layer.padding, str):
                 raise TypeError(f"unfold() padding must be a tuple of ints, got {layer.padding!r}")
-            x = forward.detach()
+            # only data pointers are read (no detach()); the records themselves are kept
+            # when already contiguous, so later updates can take the fast path
+            x, g = forward, backward
             if x.dim() != 4:
                 raise RuntimeError(f"Conv2d KFAC expects a 4-D (B,C,H,W) input, got {tuple(x.shape)}")
-            x = x.contiguous()
-            g = backward.detach().contiguous()
+            if not x.is_contiguous():
+                x = x.contiguous()
+            if not g.is_contiguous():
+                g = g.contiguous()
             opA = N.patch_operand(x, layer.kernel_size, layer.padding, layer.stride, has_bias)
             opG = N.channel_operand(g)
             keep = (x, g)

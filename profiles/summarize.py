@@ -59,9 +59,11 @@ def main(tag):
                        "mean over the bench's launches (15 updates per pass, last batch short)"}
         with open(os.path.join(dst, "factor_tiles_hbm.json"), "w") as f:
             json.dump(out, f, indent=1)
-        if "_" not in tag:  # the headline (MLP) profile: the file bench.py reads
-            with open(os.path.join(ROOT, "profiles", "factor_tiles_pmc.json"), "w") as f:
-                json.dump(out, f, indent=1)
+        # the files bench.py reads: factor_tiles_pmc.json for the headline (MLP) profile,
+        # factor_tiles_pmc_<config>.json for r02_<config> etc.
+        name = "factor_tiles_pmc.json" if "_" not in tag else f"factor_tiles_pmc_{tag.split('_', 1)[1]}.json"
+        with open(os.path.join(ROOT, "profiles", name), "w") as f:
+            json.dump(out, f, indent=1)
         print(json.dumps(out, indent=1))
 
 

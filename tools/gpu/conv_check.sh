@@ -1,11 +1,9 @@
+# Conv SYRK changes: factor parity tests, microbench, LeNet bench line.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_factors.py -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_factors.log 2>&1; rc=$?
-tail -2 gpurun_out/gpu_factors.log; [ $rc -eq 0 ] || { grep -E "Error|assert|FAIL|Mismatch|Max" gpurun_out/gpu_factors.log | head -30; exit $rc; }
-timeout -k 10 300 python bench.py --config lenet --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > gpurun_out/bench_lenet.log 2>&1 || exit $?
-python -c "import json; d=json.loads(open('gpurun_out/bench_lenet.log').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['breakdown'])"
-bash tools/gpu/trace_lenet.sh && python - <<'PY'
-import csv
-rows=list(csv.DictReader(open('gpurun_out/trace_lenet/run_kernel_stats.csv')))
-for r in rows[:8]: print(r['Name'][:70], r['Calls'], round(float(r['AverageNs'])/1e3,1),'us')
-PY
+timeout -k 10 400 python -u -m pytest tests/test_gpu_factors.py tests/test_gpu_golden_r02.py tests/test_gpu_invert.py -x -q --timeout 200 --timeout-method thread > gpurun_out/conv_tests.log 2>&1 || { tail -30 gpurun_out/conv_tests.log; exit 1; }
+tail -1 gpurun_out/conv_tests.log
+(cd tools/microbench && timeout -k 10 120 ./conv_ab > ../../gpurun_out/conv_ab.log 2>&1) || { tail gpurun_out/conv_ab.log; exit 1; }
+grep "us  (" gpurun_out/conv_ab.log | cut -c1-80
+timeout -k 10 300 python bench.py --config lenet --no-cpu-baseline --no-e2e > gpurun_out/bench_lenet2.log 2>&1 || { tail -5 gpurun_out/bench_lenet2.log; exit 1; }
+python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; b=d['breakdown']; print(sys.argv[1], '%.3e'%d['value'], 'ms/step %.3f'%d['ms_per_step'], 'host %.3f'%b['host_issue_ms_per_step'], 'tiles %.3f inv %.3f'%(b['factor_tiles_ms_per_step'], b['invert_ms_per_step']), 'frac %.3f'%r['frac'], 'serial %.3e'%(d['serial_images_per_s'] or 0))" gpurun_out/bench_lenet2.log
