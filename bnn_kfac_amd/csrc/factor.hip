@@ -527,6 +527,7 @@ constexpr int CONV_CB = 2;  // 32x32 blocks per wave (mode 0): 4*CONV_CB per wor
 
 struct ConvGeom {
   int mode;        // 0: 64x64 tiles, 1: narrow 32x32, 2: narrow 16x16
+  int n;           // factor order
   int KR;          // k-lanes per MFMA (2 or 4)
   int B;           // images of the batch
   int T;           // MFMAs along one row group (PATCH: Wo; CHANNEL: segment length Q)
@@ -797,6 +798,90 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args,
   }
 }
 
+// Channel-major factors with n <= 8 (the G of a conv layer with few output
+// channels, e.g. LeNet-5's conv1: 6): F = sum over (image, position) of g g^T is
+// n(n+1)/2 FMAs per position against n loads -- an HBM stream, not MFMA work.  Each
+// thread takes runs of 4 positions of the task's images (float4 loads, coalesced
+// along positions, no LDS staging), keeps the lower triangle in registers, and the
+// workgroup sums it in a fixed order (wave shuffles, then the 4 waves) into the
+// same 16x16 slab / accumulator block the MFMA kernel writes.  (n = 9..16 stays on
+// the MFMA kernel: 136 partial sums per thread cost more to reduce than they save.)
+template <int NMAX>
+__global__ __launch_bounds__(NTHREADS) void kfac_factor_channel_small(FactorArgs args, ConvGeom cg) {
+  constexpr int NT = NMAX * (NMAX + 1) / 2;
+  __shared__ float part[NTHREADS / 64][NT];
+  const int task = xcd_task(blockIdx.x, gridDim.x);
+  int jx = 0;
+  while (jx + 1 < args.njobs && task >= args.task_end[jx]) ++jx;
+  const FactorJobDev& J = args.job[jx];
+  const OpDev& op = J.x;
+  const int split = task - J.task_begin;  // one unit: task = split
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = op.cols;
+  const int64_t b0 = (int64_t)split * cg.B / J.splits, b1 = (int64_t)(split + 1) * cg.B / J.splits;
+  const int64_t L4 = op.L >> 2, per = (b1 - b0) * L4;  // (image, 4-position run) pairs
+  float acc[NT];
+#pragma unroll
+  for (int e = 0; e < NT; ++e) acc[e] = 0.f;
+  const float* base = op.ptr + b0 * op.sB;
+  int64_t img = tid / L4, r4 = tid - img * L4;
+  const int64_t dimg = NTHREADS / L4, dr = NTHREADS - dimg * L4;
+  for (int64_t q = tid; q < per; q += NTHREADS) {
+    const float* src = base + img * op.sB + 4 * r4;
+    floatx4 x[NMAX];
+#pragma unroll
+    for (int c = 0; c < NMAX; ++c) {
+      if (c < n) x[c] = *reinterpret_cast<const floatx4*>(src + c * op.L);
+      else x[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0, e = 0; i < NMAX; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j, ++e) acc[e] = fmaf(x[i][u], x[j][u], acc[e]);
+    img += dimg;
+    r4 += dr;
+    if (r4 >= L4) {
+      r4 -= L4;
+      ++img;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < NT; ++e) {
+    float v = acc[e];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) part[wave][e] = v;
+  }
+  __syncthreads();
+  float* out = J.slab + (size_t)split * TILE * TILE;  // block 0 of tile 0
+  for (int e = tid; e < NT; e += NTHREADS) {
+    int i = 0;
+    while ((i + 1) * (i + 2) / 2 <= e) ++i;
+    const int j = e - i * (i + 1) / 2;
+    const float t = (part[0][e] + part[1][e]) + (part[2][e] + part[3][e]);
+    float* at1 = &out[i * TILE + j];
+    float* at2 = &out[j * TILE + i];
+    if (!J.accum) {
+      *at1 = t;
+      *at2 = t;
+    } else {
+      const float v = J.sbeta == 0.f ? J.alpha * t : fmaf(J.sbeta, *at1, J.alpha * t);
+      *at1 = v;
+      *at2 = v;
+    }
+  }
+}
+
+// KFAC_CONV_SMALL=0: channel factors with n <= 8 on the MFMA kernel (A/B checks)
+static bool conv_small_off() {
+  static const bool off = [] {
+    const char* v = getenv("KFAC_CONV_SMALL");
+    return v && v[0] == '0';
+  }();
+  return off;
+}
+
 // Geometry of a conv job on the LDS-staged kernel; false: the job takes the
 // register-staged path (images too large, channel blocks not float4-shaped, a
 // multi-batch job, or an empty batch).
@@ -807,6 +892,7 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
     return false;
   const int n = o.cols + (o.has_ones ? 1 : 0);
   g = ConvGeom{};
+  g.n = n;
   g.mode = n <= 16 ? 2 : (n <= 32 ? 1 : 0);
   g.KR = g.mode == 2 ? 4 : 2;
   g.B = (int)(o.rows / o.L);
@@ -869,6 +955,10 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
 
 template <int LAYOUT>
 static void launch_conv(const FactorArgs& args, const ConvGeom& g, int tasks, hipStream_t stream) {
+  if (LAYOUT == KFAC_CHANNEL && g.n <= 8 && !conv_small_off()) {
+    hipLaunchKernelGGL(kfac_factor_channel_small<8>, dim3(tasks), dim3(NTHREADS), 0, stream, args, g);
+    return;
+  }
   const size_t shmem = (size_t)g.lds * sizeof(float);
   const bool s1 = g.stride == 1;
   const int pm = (int)cdiv(g.src, NTHREADS);  // <= 8 by CONV_SRC_MAX
@@ -1051,7 +1141,10 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
       // workgroups than another finished later (LeNet-5, batch 1024: conv2 A 68 us at
       // 400 splits -> 53 us at k = 2 (1,024 tasks); conv1 A 34 -> 27 us at k = 1;
       // tools/microbench/conv_ab.hip, KFAC_CONV_K overrides k)
-      int k = (int)std::max<int64_t>(1, cdiv((int64_t)cg.units * cg.B, slots));
+      // (the n <= 8 channel kernel: half the slots -- its per-task reduction is the
+      // larger cost there: conv1 G 15.7 / 12.4 / 13.2 us at k = 1 / 2 / 4)
+      const bool small = jobs[i].x.layout == KFAC_CHANNEL && cg.n <= 8 && !conv_small_off();
+      int k = (int)std::max<int64_t>(1, cdiv((int64_t)cg.units * cg.B, small ? slots / 2 : slots));
       static const int env_k = [] {
         const char* v = getenv("KFAC_CONV_K");
         return v ? atoi(v) : 0;
