@@ -244,8 +244,8 @@ def main(argv=None):
     ap.add_argument("--no-serial", action="store_true")
     ap.add_argument("--launch-first", type=int, default=None,
                     help="queued updates in a pass's first SYRK launch (KFAC.launch_first)")
-    ap.add_argument("--sync-invert", action="store_true",
-                    help="KFAC.async_invert = False (phase 1 of each inversion issued by the caller)")
+    ap.add_argument("--async-invert", action="store_true",
+                    help="KFAC.async_invert = True (phase 1 of each inversion issued by a worker thread)")
     ap.add_argument("--launch-idle", action="store_true",
                     help="KFAC.launch_policy = 'idle' (launch when the stream drains)")
     ap.add_argument("--partition", type=int, default=0,
@@ -298,8 +298,8 @@ def main(argv=None):
         kfac.launch_first = args.launch_first
     if args.launch_idle:
         kfac.launch_policy = "idle"
-    if args.sync_invert:
-        kfac.async_invert = False
+    if args.async_invert:
+        kfac.async_invert = True
     if args.single_buffer:
         kfac.double_buffer = False
     recs = synthetic_records(specs, images, device, seed=1234 + rank)

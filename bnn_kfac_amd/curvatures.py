@@ -219,10 +219,12 @@ class KFAC(Curvature):
         self._inv_pending = None  # (event, host info, layers, inv_state dict, outputs, on side
                                   # stream) until settled
         self.overlap_invert = True  # invert() on a side stream (see invert)
-        # with overlap_invert: the inversion's step launches (phase 1 of
-        # kfac_invert_phase, ~25 launches) are issued by a worker thread, so the
-        # caller's next update() reaches the GPU ~0.1 ms sooner
-        self.async_invert = True
+        # opt-in with overlap_invert: the inversion's step launches (phase 1 of
+        # kfac_invert_phase) issued by a worker thread.  Off by default since the
+        # merged step chain replays from a hipGraph (one call): the worker then saved
+        # no host time and its GIL hand-offs made the host's issue time jittery
+        # (MLP line 0.52-0.64 ms of host per step with it, 0.52-0.53 without)
+        self.async_invert = False
         self._inv_exec = None
         self._inv_streams = {}    # device index -> side stream
         # CU partition (opt-in; overlap_invert only; 0 = none): the inversion stream is

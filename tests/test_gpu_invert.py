@@ -147,8 +147,8 @@ def test_invert_identity_property_wide(hip_device):
     assert np.abs(E - np.eye(n)).max() < 1e-3
 
 
-@pytest.mark.parametrize("reset", [True, False])
-def test_overlapped_inversion_matches_serial(hip_device, reset):
+@pytest.mark.parametrize("reset,async_invert", [(True, False), (False, False), (True, True)])
+def test_overlapped_inversion_matches_serial(hip_device, reset, async_invert):
     """invert() runs on the side stream and the next pass is queued right behind it
     (the bench's pattern: nothing read in between, so pass k+1's SYRK overlaps
     inversion k).  With reset() the passes alternate two packed buffers and pass
@@ -168,6 +168,7 @@ def test_overlapped_inversion_matches_serial(hip_device, reset):
     def run(overlap):
         kfac = KFAC(net)
         kfac.overlap_invert = overlap
+        kfac.async_invert = async_invert  # (opt-in worker thread for phase 1)
         kfac.partition_cus = 0  # one stream layout: same SYRK splits as the serial path
         kept = []
         for batches in passes:

@@ -7,6 +7,6 @@ summ() { python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip
 for rep in 1 2; do
   KFAC_INV_GRAPH=0 timeout -k 10 200 python bench.py --no-cpu-baseline --no-e2e > gpurun_out/g0.log 2>&1 || exit 1; summ gpurun_out/g0.log
   timeout -k 10 200 python bench.py --no-cpu-baseline --no-e2e > gpurun_out/g1.log 2>&1 || exit 1; summ gpurun_out/g1.log
-  timeout -k 10 200 python bench.py --no-cpu-baseline --no-e2e --sync-invert > gpurun_out/g1s.log 2>&1 || exit 1; summ gpurun_out/g1s.log
-  timeout -k 10 200 python bench.py --no-cpu-baseline --no-e2e --sync-invert --launch-first 16 > gpurun_out/g1s16.log 2>&1 || exit 1; summ gpurun_out/g1s16.log
+  timeout -k 10 200 python bench.py --no-cpu-baseline --no-e2e --async-invert > gpurun_out/g1s.log 2>&1 || exit 1; summ gpurun_out/g1s.log
+  timeout -k 10 200 python bench.py --no-cpu-baseline --no-e2e --async-invert --launch-first 16 > gpurun_out/g1s16.log 2>&1 || exit 1; summ gpurun_out/g1s16.log
 done

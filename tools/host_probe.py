@@ -19,11 +19,12 @@ def main():
     layers = [m for m in net.modules() if isinstance(m, torch.nn.Linear)]
     recs = bench.synthetic_records(specs, 60000, dev, seed=0)
     kfac = KFAC(net)
-    if len(sys.argv) > 1 and sys.argv[1] == "sync":
-        kfac.async_invert = False
+    if len(sys.argv) > 1 and sys.argv[1] == "async":
+        kfac.async_invert = True
     starts = list(range(0, 60000, 4096))
     T = {"reset": 0.0, "update": 0.0, "invert": 0.0, "record": 0.0}
     upd = []
+    per_idx = {}
 
     def one_pass(meas):
         t = time.perf_counter()
@@ -39,6 +40,7 @@ def main():
                 T["record"] += t2 - t1
                 T["update"] += t3 - t2
                 upd.append(t3 - t2)
+                per_idx.setdefault(i // 4096, []).append(t3 - t2)
             t1 = t3
         t4 = time.perf_counter()
         kfac.invert(0.04, 200)
@@ -64,9 +66,11 @@ def main():
     upd.sort()
     print(f"update(): median {1e6 * upd[len(upd) // 2]:.1f} us, p90 {1e6 * upd[int(0.9 * len(upd))]:.1f} us, "
           f"max {1e6 * upd[-1]:.1f} us")
+    print("update() by index in the pass (median us): " + " ".join(
+        f"{k}:{1e6 * sorted(v)[len(v) // 2]:.0f}" for k, v in sorted(per_idx.items())))
 
 
-if __name__ == "__main__" and (len(sys.argv) < 2 or sys.argv[1] != "launch"):
+if __name__ == "__main__" and (len(sys.argv) < 2 or sys.argv[1] not in ("launch", "invert", "parts")):
     main()
 
 
@@ -119,3 +123,103 @@ def probe_launch():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "launch":
     probe_launch()
+
+
+def probe_invert():
+    """cProfile of invert() in the pipelined loop (GPU busy, no syncs)."""
+    import cProfile
+    import pstats
+    dev = torch.device("cuda:0")
+    torch.cuda.set_stream(torch.cuda.Stream(dev))
+    specs = bench.CONFIGS["mlp"]
+    net = bench.build_model("mlp", dev)
+    layers = [m for m in net.modules() if isinstance(m, torch.nn.Linear)]
+    recs = bench.synthetic_records(specs, 60000, dev, seed=0)
+    kfac = KFAC(net)
+    starts = list(range(0, 60000, 4096))
+    pr = cProfile.Profile()
+
+    def one_pass(meas):
+        kfac.reset()
+        for i in starts:
+            for layer, (a, g) in zip(layers, recs):
+                kfac.record[layer] = [a[i:i + 4096], g[i:i + 4096]]
+            kfac.update(batch_size=min(4096, 60000 - i))
+        if meas:
+            pr.enable()
+        kfac.invert(0.04, 200)
+        if meas:
+            pr.disable()
+
+    for _ in range(5):
+        one_pass(False)
+    for _ in range(20):
+        one_pass(True)
+    kfac.inv_state
+    torch.cuda.synchronize()
+    pstats.Stats(pr).sort_stats("tottime").print_stats(18)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "invert":
+    probe_invert()
+
+
+def probe_invert_parts():
+    """Wall time of invert()'s parts (pipelined loop): each wrapped call's total."""
+    from bnn_kfac_amd import _native as N
+    from bnn_kfac_amd import curvatures as CV
+    dev = torch.device("cuda:0")
+    torch.cuda.set_stream(torch.cuda.Stream(dev))
+    specs = bench.CONFIGS["mlp"]
+    net = bench.build_model("mlp", dev)
+    layers = [m for m in net.modules() if isinstance(m, torch.nn.Linear)]
+    recs = bench.synthetic_records(specs, 60000, dev, seed=0)
+    kfac = KFAC(net)
+    starts = list(range(0, 60000, 4096))
+    acc = {}
+    on = [False]
+
+    def wrap(obj, name):
+        f = getattr(obj, name)
+
+        def g(*a, **k):
+            t = time.perf_counter()
+            try:
+                return f(*a, **k)
+            finally:
+                if on[0]:
+                    acc[name] = acc.get(name, 0.0) + time.perf_counter() - t
+        setattr(obj, name, g)
+
+    for nm in ("invert_prepare", "invert_phase", "factor_flush", "invert_job"):
+        wrap(N, nm)
+    for nm in ("_defer_verdict", "_damping", "_side_stream", "_release", "_invert_async", "flush"):
+        wrap(kfac, nm)
+    tot = [0.0]
+
+    def one_pass(meas):
+        kfac.reset()
+        for i in starts:
+            for layer, (a, g) in zip(layers, recs):
+                kfac.record[layer] = [a[i:i + 4096], g[i:i + 4096]]
+            kfac.update(batch_size=min(4096, 60000 - i))
+        on[0] = meas
+        t = time.perf_counter()
+        kfac.invert(0.04, 200)
+        if meas:
+            tot[0] += time.perf_counter() - t
+        on[0] = False
+
+    for _ in range(5):
+        one_pass(False)
+    n = 20
+    for _ in range(n):
+        one_pass(True)
+    kfac.inv_state
+    torch.cuda.synchronize()
+    print(f"invert(): {1e6 * tot[0] / n:.1f} us per call; " +
+          ", ".join(f"{k} {1e6 * v / n:.1f}" for k, v in sorted(acc.items(), key=lambda kv: -kv[1])))
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "parts":
+    probe_invert_parts()
