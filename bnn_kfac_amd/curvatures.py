@@ -204,10 +204,14 @@ class KFAC(Curvature):
         self._queue = []         # per queued update: (jobs, operand pointers, kept records,
                                  # their _version, device, merge key)
         # launch sizes: the first launch of a pass takes `launch_first` queued updates,
-        # each later one twice as many (up to defer_batches)
-        self.launch_first = 1
+        # each later one twice as many (up to defer_batches; defer_bytes caps them
+        # too).  1: the GPU starts on a pass while the host is still issuing it.  16
+        # (a pass of <= 16 updates = one launch at the flush) measured +1.5 % on the
+        # pipelined MLP line, +2.7 % LeNet-5, +0.4 % wide, but -12 % on the serial
+        # pass-then-invert loop the reference's scripts run (the host's issue of the
+        # pass is no longer overlapped): kept at 1.
+        self.launch_first = 1    # (property: also restarts the doubling)
         self.launch_policy = "double"
-        self._launch_at = self.launch_first  # queue length that triggers the next launch
         self._fast = None        # job templates of the last slow-path update (see _remember)
         self._acc_buf = None     # device buffer of the accumulators
         self._acc_map = None     # F pointer -> (acc pointer, splits) of the pending cycle
@@ -418,6 +422,15 @@ class KFAC(Curvature):
         nA = opA.cols + opA.has_ones
         nG = opG.cols
         return opA, opG, nA, nG, keep
+
+    @property
+    def launch_first(self) -> int:
+        return self._launch_first
+
+    @launch_first.setter
+    def launch_first(self, value: int):
+        self._launch_first = int(value)
+        self._launch_at = self._launch_first  # queue length that triggers the next launch
 
     def _alpha(self, op: N.Operand) -> float:
         """Per-batch mean: 1/cols (curvatures.py:349,356); an empty batch gives
@@ -654,12 +667,15 @@ class KFAC(Curvature):
             self._acc_live.add(j.F)
 
     # ------------------------------------------------------------------ invert
-    def _damping(self, add, multiply):
-        """curvatures.py:373-378 argument handling, per state entry."""
+    def _damping(self, add, multiply, count=None):
+        """curvatures.py:373-378 argument handling, per state entry (`count`: the
+        number of state entries, when the caller already holds them)."""
+        if count is None:
+            count = len(self.state)
         out = []
-        for index in range(len(self.state)):
+        for index in range(count):
             if not isinstance(add, (float, int)) and not isinstance(multiply, (float, int)):
-                assert len(add) == len(multiply) == len(self.state)
+                assert len(add) == len(multiply) == count
                 n, s = add[index], multiply[index]
             else:
                 n, s = float(add), float(multiply)
@@ -668,14 +684,15 @@ class KFAC(Curvature):
 
     def invert(self, add: Union[float, list, tuple] = 0., multiply: Union[float, list, tuple] = 1.):
         """L = cholesky(inverse(sqrt(s) F + sqrt(n) I)) per factor (curvatures.py:367-398)."""
-        assert self.state, "State dict is empty. Did you call 'update' prior to this?"
+        state = self.state  # (one flush: `state` completes the deferred reduction)
+        assert state, "State dict is empty. Did you call 'update' prior to this?"
         # the previous inversion's verdict is read later (no host wait here): its
         # outputs are ordered before later work on the caller's stream now
         self._defer_verdict()
         if self._inv_state:
             Warning("State has already been inverted. Is this expected?")
-        damping = self._damping(add, multiply)
-        entries = list(self.state.items())
+        entries = list(state.items())
+        damping = self._damping(add, multiply, len(entries))
         for layer, (first, second) in entries:
             N.require_device(first, "state", layer)
             N.require_device(second, "state", layer)

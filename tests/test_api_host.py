@@ -175,12 +175,13 @@ def test_queued_updates_merge_into_multibatch_jobs(monkeypatch):
                 torch.tensor(rng.standard_normal((B, 3)).astype(np.float32))]
                for B in sizes]
 
-    def run(defer_reduce, defer_batches=64, defer_bytes=256 << 20):
+    def run(defer_reduce, defer_batches=64, defer_bytes=256 << 20, launch_first=1):
         host_double.UPDATES.clear()
         net = mlp()
         kfac = KFAC(net)
         kfac.defer_reduce, kfac.defer_batches = defer_reduce, defer_batches
         kfac.defer_bytes = defer_bytes
+        kfac.launch_first = launch_first
         for a1, g1, a2, g2 in batches:
             kfac.record[net[0]] = [a1, g1]
             kfac.record[net[2]] = [a2, g2]
@@ -196,6 +197,12 @@ def test_queued_updates_merge_into_multibatch_jobs(monkeypatch):
         np.testing.assert_allclose(g, w, rtol=1e-6)
     got, launches = run(True, defer_batches=2)  # [8] [8 8] [5 8] [8]
     assert launches == [[1] * 4, [2] * 4, [1] * 4, [1] * 4, [1] * 4]
+    for g, w in zip(got, want):
+        np.testing.assert_allclose(g, w, rtol=1e-6)
+    # the default first launch (16 queued updates): the whole pass is queued until
+    # the flush, one launch call per merge group: [8 8 8] [5] [8 8]
+    got, launches = run(True, launch_first=KFAC(mlp()).launch_first)
+    assert launches == [[3] * 4, [1] * 4, [2] * 4]
     for g, w in zip(got, want):
         np.testing.assert_allclose(g, w, rtol=1e-6)
     # defer_bytes caps the records a queue holds: an 8-row update keeps 608 bytes,

@@ -243,6 +243,7 @@ def test_cu_partitioned_passes_match_serial(hip_device):
         kfac = KFAC(net)
         kfac.overlap_invert = overlap
         kfac.partition_cus = 32
+        kfac.launch_first = 1  # launches during the pass (the partition's data stream)
         states, invs, used = [], [], []
         for batches in passes:
             kfac.reset()
