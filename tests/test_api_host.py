@@ -199,9 +199,9 @@ def test_queued_updates_merge_into_multibatch_jobs(monkeypatch):
     assert launches == [[1] * 4, [2] * 4, [1] * 4, [1] * 4, [1] * 4]
     for g, w in zip(got, want):
         np.testing.assert_allclose(g, w, rtol=1e-6)
-    # the default first launch (16 queued updates): the whole pass is queued until
-    # the flush, one launch call per merge group: [8 8 8] [5] [8 8]
-    got, launches = run(True, launch_first=KFAC(mlp()).launch_first)
+    # a first launch of 16 queued updates: the whole pass is queued until the flush,
+    # one launch call per merge group: [8 8 8] [5] [8 8]
+    got, launches = run(True, launch_first=16)
     assert launches == [[3] * 4, [1] * 4, [2] * 4]
     for g, w in zip(got, want):
         np.testing.assert_allclose(g, w, rtol=1e-6)
