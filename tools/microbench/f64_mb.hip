@@ -8,6 +8,7 @@
 //   rowi  block row w, k-major: per k0 one A fragment, 4 B fragments, 4 MFMAs
 //   quad  wave w owns a 2x2 block square, k-major: 2 A + 2 B fragments per 4 MFMAs
 //   rowR / regR: row / reg with random full-mantissa operands (power-limited clock)
+//   glob / pipe / g128: the inv_bulk shape with global tiles (see k_glob, k_pipe, k_glob128)
 // plus the pure-register issue ceilings (no LDS, no barriers) of the f64 16x16x4 and
 // the f32 32x32x2 / 16x16x4 MFMAs with 1 or 4 independent accumulator chains per wave.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o f64_mb f64_mb.hip
@@ -262,6 +263,84 @@ static void run_glob(double* W, int T, int S, int tmod) {
          flop / (t[2] * 1e-3) / 1e12);
 }
 
+// 128 x 128 output per workgroup (4 waves, each a 64 x 64 quadrant = 4 x 4 blocks of
+// 16 x 16, 16 accumulators), one 128 x 64 A and B panel pair in LDS per 64-wide step
+// (135 KB: 1 workgroup per CU), tiles loaded global -> registers -> LDS.  Grid cycles
+// over the lower triangle of 128-tiles of rows/cols >= S.
+constexpr int MB = 128;
+__global__ __launch_bounds__(NT, 1) void k_glob128(double* W, int Np, int S, int m) {
+  extern __shared__ double sh[];
+  double* A = sh;
+  double* B = sh + MB * DP;
+  const int tb = blockIdx.x % (m * (m + 1) / 2);
+  int a = (int)((sqrtf(8.f * tb + 1.f) - 1.f) * 0.5f);
+  while ((a + 1) * (a + 2) / 2 <= tb) ++a;
+  while (a * (a + 1) / 2 > tb) --a;
+  const int b = tb - a * (a + 1) / 2;
+  const size_t i0 = (size_t)S * NB + (size_t)a * MB, j0 = (size_t)S * NB + (size_t)b * MB;
+  const int c = threadIdx.x % NB, r0 = threadIdx.x / NB;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, li = lane & 15, kk = lane >> 4;
+  const int wr = (w >> 1) * 64, wc = (w & 1) * 64;
+  doublex4 acc[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) acc[x][y] = doublex4{0, 0, 0, 0};
+  for (int k = 0; k < S; ++k) {
+    const double* ga = W + i0 * Np + k * NB;
+    const double* gb = W + j0 * Np + k * NB;
+#pragma unroll
+    for (int q = 0; q < MB / 4; ++q) {  // 32 rows per pass of 4: 32 loads each
+      A[(r0 + 4 * q) * DP + c] = ga[(size_t)(r0 + 4 * q) * Np + c];
+      B[(r0 + 4 * q) * DP + c] = gb[(size_t)(r0 + 4 * q) * Np + c];
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int k0 = 0; k0 < NB; k0 += 4) {
+      double av[4], bv[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        av[x] = A[(wr + 16 * x + li) * DP + k0 + kk];
+        bv[x] = B[(wc + 16 * x + li) * DP + k0 + kk];
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = mf(av[x], bv[y], acc[x][y]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        double* p = W + (i0 + wr + 16 * x + (lane >> 4) + 4 * v) * Np + j0 + wc + 16 * y + (lane & 15);
+        *p = *p - acc[x][y][v];
+      }
+}
+
+static void run_glob128(double* W, int T, int S) {
+  const int Np = T * NB, m = (T - S) * NB / MB, grid = 2048;
+  const int shmem = 2 * MB * DP * sizeof(double);
+  (void)hipFuncSetAttribute((const void*)k_glob128, hipFuncAttributeMaxDynamicSharedMemorySize, shmem);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+  std::vector<float> t;
+  for (int rep = 0; rep < 5; ++rep) {
+    (void)hipEventRecord(e0, 0);
+    hipLaunchKernelGGL(k_glob128, dim3(grid), dim3(NT), shmem, 0, W, Np, S, m);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms; (void)hipEventElapsedTime(&ms, e0, e1);
+    t.push_back(ms);
+  }
+  std::sort(t.begin(), t.end());
+  const double flop = 2.0 * MB * MB * NB * (double)S * grid;
+  printf("g128  T %d S %2d grid %5d  %8.3f ms  %6.2f TF/s fp64\n", T, S, grid, t[2], flop / (t[2] * 1e-3) / 1e12);
+}
+
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 // KIND 0: f64 16x16x4, 1: f32 32x32x2, 2: f32 16x16x4; CH independent chains; R x 16 MFMAs each
@@ -362,6 +441,9 @@ int main() {
     run_glob(W, T, 8);
     run_glob(W, T, 16);
     run_glob(W, T, 8, 12);  // tiles mod 12: a 4.7 MB working set
+    run_glob128(W, T, 4);
+    run_glob128(W, T, 8);
+    run_glob128(W, T, 16);
     run_pipe<false>(W, T, 4);
     run_pipe<false>(W, T, 8);
     run_pipe<false>(W, T, 16);
