@@ -432,210 +432,6 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, const fl
 }
 
 
-// ---------------------------------------------------------------------------
-// Barrier-free row-major SYRK (KFAC_SYRK_DIRECT=CH).  Same tasks, slabs and
-// reduce as the LDS-DMA path, but each WAVE owns the whole 64x64 tile over a
-// contiguous quarter of the task's stage range and loads its MFMA operands
-// straight from global memory (L2) into registers, one chunk of CH row pairs
-// ahead: no LDS ring, no per-stage barrier, so the 16 waves of a CU run
-// independently instead of in per-stage lockstep.  Per row pair a wave issues
-// 2 (diagonal) or 4 dword loads (32 consecutive floats per half-wave, one
-// 128-byte line) against 3 or 4 v_mfma_f32_32x32x2f32 -- the same operand bytes
-// per flop as the workgroup-shared LDS panels (a 64x64 tile reads 128 floats
-// per row either way).  The four waves' partial tiles are summed through LDS in
-// a fixed order (w0 + w2) + (w1 + w3) before the slab store: deterministic.
-// Block (i, j) of the tile = rows 32i.., columns 32j..; VAR selects the blocks:
-enum DirVar { DV_FULL = 0, DV_ROW_EDGE = 1, DV_DIAG = 2, DV_DIAG_EDGE = 3 };
-//   FULL      (0,0) (0,1) (1,0) (1,1)   off-diagonal tile
-//   ROW_EDGE  (0,0) (0,1)               off-diagonal, rows 32.. past n
-//   DIAG      (0,0) (1,0) (1,1)         diagonal tile (B panel = A panel)
-//   DIAG_EDGE (0,0)                     diagonal, rows/cols 32.. past n (and n <= 32)
-template <int VAR> struct DirBlocks {
-  static constexpr bool diag = VAR >= DV_DIAG;
-  static constexpr bool a1 = VAR == DV_FULL || VAR == DV_DIAG;  // A rows 32..63 live
-  static constexpr bool b1 = VAR <= DV_ROW_EDGE;                // B cols 32..63 live (off-diag)
-};
-
-struct DirCol {  // one lane's column of one 32-column block
-  int col;       // column read (0 when the lane holds no matrix data: a safe address)
-  bool real;     // column < cols
-  float fill;    // value of a non-real column (the bias ones column: 1)
-  __device__ __forceinline__ void init(const OpDev& op, int c) {
-    real = c < op.cols;
-    col = real ? c : 0;
-    fill = c == op.ones ? 1.f : 0.f;
-  }
-};
-
-template <int CH>
-struct DirChunk {
-  float a0[CH], a1[CH], b0[CH], b1[CH];
-};
-
-// rows k0 + 2p + h (p < CH) of the batch at `base`; rows >= lim (relative) are zero
-template <int CH, int VAR>
-__device__ __forceinline__ void dir_load(DirChunk<CH>& d, const float* base, int64_t k0, int64_t ld,
-                                         int64_t lim, int h, const DirCol (&ca)[2], const DirCol (&cb)[2]) {
-  using V = DirBlocks<VAR>;
-  const float* r = base + (k0 + h) * ld;
-  if (lim >= 2 * CH) {
-#pragma unroll
-    for (int p = 0; p < CH; ++p) {
-      const float* rp = r + 2 * p * ld;
-      const float x0 = rp[ca[0].col];
-      d.a0[p] = ca[0].real ? x0 : ca[0].fill;
-      if (V::a1) {
-        const float x1 = rp[ca[1].col];
-        d.a1[p] = ca[1].real ? x1 : ca[1].fill;
-      }
-      if (!V::diag) {
-        const float y0 = rp[cb[0].col];
-        d.b0[p] = cb[0].real ? y0 : cb[0].fill;
-        if (V::b1) {
-          const float y1 = rp[cb[1].col];
-          d.b1[p] = cb[1].real ? y1 : cb[1].fill;
-        }
-      }
-    }
-  } else {
-#pragma unroll
-    for (int p = 0; p < CH; ++p) {
-      const bool ok = 2 * p + h < lim;
-      const float* rp = r + 2 * p * ld;
-      d.a0[p] = ok ? (ca[0].real ? rp[ca[0].col] : ca[0].fill) : 0.f;
-      if (V::a1) d.a1[p] = ok ? (ca[1].real ? rp[ca[1].col] : ca[1].fill) : 0.f;
-      if (!V::diag) {
-        d.b0[p] = ok ? (cb[0].real ? rp[cb[0].col] : cb[0].fill) : 0.f;
-        if (V::b1) d.b1[p] = ok ? (cb[1].real ? rp[cb[1].col] : cb[1].fill) : 0.f;
-      }
-    }
-  }
-}
-
-template <int CH, int VAR>
-__device__ __forceinline__ void dir_mma(const DirChunk<CH>& d, floatx16 (&acc)[4]) {
-  using V = DirBlocks<VAR>;
-#pragma unroll
-  for (int p = 0; p < CH; ++p) {
-    const float b0 = V::diag ? d.a0[p] : d.b0[p];
-    const float b1 = V::diag ? d.a1[p] : d.b1[p];
-    acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(d.a0[p], b0, acc[0], 0, 0, 0);
-    if (V::b1) acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(d.a0[p], b1, acc[1], 0, 0, 0);
-    if (V::a1) acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(d.a1[p], b0, acc[2], 0, 0, 0);
-    if (V::a1 && (V::b1 || V::diag))
-      acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(d.a1[p], b1, acc[3], 0, 0, 0);
-  }
-}
-
-// one wave's contraction over stages [w0, w1) of job J (chunks of 2*CH rows; a
-// stage of BK rows never straddles two batches, so neither does a chunk)
-template <int CH, int VAR>
-__device__ __forceinline__ void dir_wave(const FactorJobDev& J, const float* const* segs, int64_t w0,
-                                         int64_t w1, int ti, int tj, floatx16 (&acc)[4]) {
-  static_assert(BK % (2 * CH) == 0, "a stage is a whole number of chunks");
-  constexpr int CPS = BK / (2 * CH);
-  const int lane = threadIdx.x & 63, h = lane >> 5, rr = lane & 31;
-  DirCol ca[2], cb[2];
-  ca[0].init(J.x, ti * TILE + rr);
-  ca[1].init(J.x, ti * TILE + 32 + rr);
-  cb[0].init(J.x, tj * TILE + rr);
-  cb[1].init(J.x, tj * TILE + 32 + rr);
-  const int64_t nch = (w1 - w0) * CPS;
-  if (nch <= 0) return;
-  const int64_t rows = J.x.rows, ld = J.x.ld;
-  StageCursor c;
-  c.init(J, w0);
-  int sub = 0;
-  const float* base = seg_base(J, segs, c.seg);
-  DirChunk<CH> cur, nxt;
-  int64_t k0 = c.k;
-  dir_load<CH, VAR>(cur, base, k0, ld, rows - k0, h, ca, cb);
-  for (int64_t i = 0; i < nch; ++i) {
-    if (i + 1 < nch) {
-      if (++sub == CPS) {
-        sub = 0;
-        const int seg = c.seg;
-        c.next(rows);
-        if (c.seg != seg) base = seg_base(J, segs, c.seg);
-      }
-      k0 = c.k + sub * 2 * CH;
-      dir_load<CH, VAR>(nxt, base, k0, ld, rows - k0, h, ca, cb);
-    }
-    dir_mma<CH, VAR>(cur, acc);
-    cur = nxt;
-  }
-}
-
-template <int CH>
-__device__ __forceinline__ void factor_task_direct(const FactorJobDev& J, const float* const* segs,
-                                                   int local, float* lds, int split_major) {
-  const int ntiles = J.t * (J.t + 1) / 2;
-  const int split = split_major ? local / ntiles : local % J.splits;
-  const int tile = split_major ? local - split * ntiles : local / J.splits;
-  int ti, tj;
-  tri_decode(tile, ti, tj);
-  const int64_t s0 = (int64_t)split * J.chunk;
-  const int64_t s1 = min(J.nst, s0 + J.chunk);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t ns = s1 > s0 ? s1 - s0 : 0;
-  const int64_t w0 = s0 + ns * wave / 4, w1 = s0 + ns * (wave + 1) / 4;
-  const bool diag = ti == tj, a1 = ti * TILE + 32 < J.n;
-  const int var = diag ? (a1 ? DV_DIAG : DV_DIAG_EDGE) : (a1 ? DV_FULL : DV_ROW_EDGE);
-  // blocks written (in acc order (0,0) (0,1) (1,0) (1,1))
-  const bool live[4] = {true, !diag, a1, a1};
-  floatx16 acc[4];
-#pragma unroll
-  for (int b = 0; b < 4; ++b)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) acc[b][v] = 0.f;
-  switch (var) {
-    case DV_FULL: dir_wave<CH, DV_FULL>(J, segs, w0, w1, ti, tj, acc); break;
-    case DV_ROW_EDGE: dir_wave<CH, DV_ROW_EDGE>(J, segs, w0, w1, ti, tj, acc); break;
-    case DV_DIAG: dir_wave<CH, DV_DIAG>(J, segs, w0, w1, ti, tj, acc); break;
-    default: dir_wave<CH, DV_DIAG_EDGE>(J, segs, w0, w1, ti, tj, acc); break;
-  }
-  // fixed-order combine: (w0 + w2) + (w1 + w3), in two 16 KB-per-wave LDS rounds
-  auto put = [&](int slot) {
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-      if (live[b])
-#pragma unroll
-        for (int v = 0; v < 16; ++v) lds[((slot * 4 + b) * 16 + v) * 64 + lane] = acc[b][v];
-  };
-  auto add = [&](int slot) {
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-      if (live[b])
-#pragma unroll
-        for (int v = 0; v < 16; ++v) acc[b][v] += lds[((slot * 4 + b) * 16 + v) * 64 + lane];
-  };
-  if (wave >= 2) put(wave - 2);
-  __syncthreads();
-  if (wave < 2) add(wave);
-  __syncthreads();
-  if (wave == 1) put(0);
-  __syncthreads();
-  if (wave != 0) return;
-  add(0);
-  float* out = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE;
-#pragma unroll
-  for (int b = 0; b < 4; ++b)
-    if (live[b]) {
-      float* o = out + (b >> 1) * 32 * TILE + (b & 1) * 32;
-      put_partial(J, acc[b], [&](int v) { return &o[acc_row(v, lane) * TILE + (lane & 31)]; });
-    }
-}
-
-template <int CH, int OCC>
-__global__ __launch_bounds__(NTHREADS, OCC) void kfac_factor_tiles_direct(FactorArgs args) {
-  __shared__ __attribute__((aligned(16))) float lds[2 * 4 * 16 * 64];  // 32 KB: the combine
-  const int task = xcd_task(blockIdx.x, gridDim.x);
-  int j = 0;
-  while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
-  const FactorJobDev& J = args.job[j];
-  factor_task_direct<CH>(J, args.segs, task - J.task_begin, lds, args.split_major);
-}
-
 // One launch per grouped update.  The row-major family (FAMILY = KFAC_ROWMAJOR)
 // takes the LDS-DMA path when a job's operand allows it, else the register-staged
 // row-major path; channel-major and im2col jobs get launches (and register budgets)
@@ -1286,26 +1082,10 @@ static bool job_glds(const kfac_factor_job& jb) {
          (jb.x.ld % 4) == 0 && (reinterpret_cast<uintptr_t>(jb.x.ptr) % 16) == 0;
 }
 
-// KFAC_SYRK_DIRECT: the barrier-free row-major kernel, CH row pairs per chunk
-// (+ resident workgroups per CU as a second digit): 2 (CH 2, 4 per CU), 43 (CH 4, 3 per CU)
-static int syrk_direct() {
-  static const int d = [] {
-    const char* v = getenv("KFAC_SYRK_DIRECT");
-    const int x = v ? atoi(v) : 0;
-    return (x == 2 || x == 43) ? x : 0;
-  }();
-  return d;
-}
-
 static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
                       int64_t slots = 0) {
-  // resident workgroups per CU: 4 (32 KB of LDS each); 3 for the 3-wave direct kernels
-  if (slots <= 0) {
-    bool rowmajor = njobs > 0;
-    for (int i = 0; i < njobs; ++i) rowmajor &= jobs[i].x.layout == KFAC_ROWMAJOR;
-    const int per_cu = rowmajor && syrk_direct() > 10 ? 3 : 4;
-    slots = per_cu * (int64_t)(g_cu_budget > 0 ? g_cu_budget : 256);
-  }
+  // resident workgroups per CU: 4 (32 KB of LDS each)
+  if (slots <= 0) slots = 4 * (int64_t)(g_cu_budget > 0 ? g_cu_budget : 256);
   constexpr int64_t MIN_CHUNK = 8, OVERHEAD = 4;  // stages; ~per-task fixed cost in stages
   int64_t max_steps = 1;
   for (int i = 0; i < njobs; ++i) max_steps = std::max(max_steps, job_stages(jobs[i]));
@@ -1510,12 +1290,7 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
         {
           bool all_glds = true;
           for (int i = 0; i < njobs; ++i) all_glds &= args.job[i].glds != 0 || args.job[i].n <= 32;
-          const int direct = syrk_direct();
-          if (direct == 2)
-            hipLaunchKernelGGL((kfac_factor_tiles_direct<2, 4>), dim3(tasks), dim3(NTHREADS), 0, stream, args);
-          else if (direct == 43)
-            hipLaunchKernelGGL((kfac_factor_tiles_direct<4, 3>), dim3(tasks), dim3(NTHREADS), 0, stream, args);
-          else if (all_glds)
+          if (all_glds)
             hipLaunchKernelGGL(kfac_factor_tiles_glds, dim3(tasks), dim3(NTHREADS), 0, stream, args);
           else
             hipLaunchKernelGGL(kfac_factor_tiles, dim3(tasks), dim3(NTHREADS), 0, stream, args);
