@@ -223,6 +223,11 @@ class KFAC(Curvature):
         self._inv_pending = None  # (event, host info, layers, inv_state dict, outputs, on side
                                   # stream) until settled
         self.overlap_invert = True  # invert() on a side stream (see invert)
+        # eager_verdict (opt-in): invert() waits for its own pivot check and raises
+        # LinAlgError itself, as the reference's invert does (curvatures.py:393-396);
+        # by default the verdict is settled at the next inv_state read or invert(), so
+        # the next data pass can be queued behind the inversion without a host sync
+        self.eager_verdict = False
         # opt-in with overlap_invert: the inversion's step launches (phase 1 of
         # kfac_invert_phase) issued by a worker thread.  Off by default since the
         # merged step chain replays from a hipGraph (one call): the worker then saved
@@ -732,7 +737,10 @@ class KFAC(Curvature):
                     pair.append(out)
                 outs.append((layer, tuple(pair)))
             if read is not None and self.async_invert:
-                return self._invert_async(device, main, side, part_side, jobs, outs, read, entries)
+                self._invert_async(device, main, side, part_side, jobs, outs, read, entries)
+                if self.eager_verdict:
+                    self._check_inverse()
+                return
             info = N.invert(jobs, device, inputs_read=read)
             # The pivot verdict travels back with a non-blocking copy into pinned
             # memory; it is settled (event wait) at the next read of `inv_state` or the
@@ -760,6 +768,8 @@ class KFAC(Curvature):
             self._inv_state[layer] = pair
         self._inv_pending = (done, host, [layer for layer, _ in outs], self._inv_state,
                              [t for _, pair in outs for t in pair], side is not main, part_side, None)
+        if self.eager_verdict:
+            self._check_inverse()
 
     def _invert_async(self, device, main, side, part_side, jobs, outs, read, entries):
         """invert() with overlap_invert: phase 0 (the launches that read F) here, the

@@ -162,7 +162,9 @@ class DistributedKFAC(KFAC):
         self._sharded_last = self._shard_now(entries)
         if not self._sharded_last:
             return super().invert(add, multiply)
-        return self._invert_sharded(entries, add, multiply)
+        self._invert_sharded(entries, add, multiply)
+        if self.eager_verdict:
+            self._check_inverse()
 
     def _invert_sharded(self, entries, add, multiply):
         """Each rank inverts the factors it owns (one grouped kfac_invert on the

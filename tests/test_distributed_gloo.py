@@ -63,17 +63,22 @@ def _worker(rank, world, port, result_q, scenario):
         dist.all_reduce = orig
         out = [t.numpy().copy() for pair in kfac.state.values() for t in pair]
         inv = None
-        if scenario in ("sharded", "sharded_singular"):
-            if scenario == "sharded_singular":
+        if scenario in ("sharded", "sharded_singular", "sharded_singular_eager"):
+            if scenario.startswith("sharded_singular"):
                 # layer 1's G made indefinite: layers from the first failing one are
                 # dropped and LinAlgError raised on every rank (curvatures.py:393-396)
                 kfac.state[net[2]][1].fill_(-1.0)
             kfac.shard_inversion = True
+            kfac.eager_verdict = scenario == "sharded_singular_eager"
+            in_invert = True
             try:
                 kfac.invert(0.04, 200)
+                in_invert = False
                 inv = [t.numpy().copy() for pair in kfac.inv_state.values() for t in pair]
             except np.linalg.LinAlgError:
                 inv = ("LinAlgError", sorted(kfac._inv_state.keys(), key=id) == sorted([net[0]], key=id))
+                if kfac.eager_verdict:  # eager: raised by invert() itself, as the reference
+                    inv = inv + (in_invert,)
         result_q.put((rank, out, calls["n"], inv))
     finally:
         dist.destroy_process_group()
@@ -99,7 +104,8 @@ def _reference(scenario):
 
 @pytest.mark.parametrize("scenario,world", [("even", 2), ("uneven", 2), ("two_passes", 2),
                                             ("even", 4), ("state_read", 2), ("sharded", 2),
-                                            ("sharded", 3), ("sharded_singular", 2)])
+                                            ("sharded", 3), ("sharded_singular", 2),
+                                            ("sharded_singular_eager", 2)])
 def test_sharded_pass_matches_single_device(scenario, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -125,3 +131,5 @@ def test_sharded_pass_matches_single_device(scenario, world):
                                            rtol=1e-5, atol=1e-6)
         if scenario == "sharded_singular":
             assert inv == ("LinAlgError", True)
+        if scenario == "sharded_singular_eager":
+            assert inv == ("LinAlgError", True, True)

@@ -130,6 +130,23 @@ def test_singular_raises_linalgerror(hip_device):
     assert net[0] in kfac.inv_state
 
 
+def test_singular_eager_verdict_raises_in_invert(hip_device):
+    """KFAC.eager_verdict: invert() itself raises, as the reference's does
+    (curvatures.py:393-396), and a later good inversion still runs."""
+    from bnn_kfac_amd.curvatures import KFAC
+    g = golden("g2_singular.npz")
+    net = nn.Sequential(nn.Linear(6, 4)).to(hip_device)
+    kfac = KFAC(net)
+    kfac.eager_verdict = True
+    kfac.record[net[0]] = [_t(g["a"], hip_device), _t(g["g"], hip_device)]
+    kfac.update(2)
+    with pytest.raises(np.linalg.LinAlgError):
+        kfac.invert(0.0, 1.0)
+    assert net[0] not in kfac._inv_state
+    kfac.invert(1.0, 1.0)  # damped: positive definite, no raise
+    assert net[0] in kfac.inv_state
+
+
 def test_invert_identity_property_wide(hip_device):
     """Size-independent check at a wide-MLP-like size: L L^T R = I."""
     from bnn_kfac_amd import _native as N
