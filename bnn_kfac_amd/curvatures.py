@@ -536,6 +536,9 @@ class KFAC(Curvature):
             t.beta = 1.0
             tmpl.append(t)
         self._fast = (getattr(self, "_scale", 1.0), spec, tuple(tmpl), device)
+        # bytes of the records one fast-path update keeps queued (the signatures fix them)
+        self._fast_bytes = sum(t.numel() * t.element_size()
+                               for layer, *_ in prepared for t in self.record[layer])
 
     def _fast_entry(self):
         scale, spec, tmpl, device = self._fast
@@ -561,7 +564,9 @@ class KFAC(Curvature):
         if self._queue and self._queue[0][4] != entry[4]:
             self._launch_queue()
         self._queue.append(entry)
-        self._queue_bytes += sum(t.numel() * t.element_size() for t in entry[2])
+        fast = self._fast
+        self._queue_bytes += (self._fast_bytes if fast is not None and entry[0] is fast[2]
+                              else sum(t.numel() * t.element_size() for t in entry[2]))
         # launch policy (the records held are capped by defer_bytes either way):
         # * "double" (default): launch sizes double from `launch_first` up to
         #   defer_batches -- a function of the update count only, so the launches'
