@@ -244,12 +244,6 @@ def main(argv=None):
     ap.add_argument("--no-serial", action="store_true")
     ap.add_argument("--launch-first", type=int, default=None,
                     help="queued updates in a pass's first SYRK launch (KFAC.launch_first)")
-    ap.add_argument("--async-invert", action="store_true",
-                    help="KFAC.async_invert = True (phase 1 of each inversion issued by a worker thread)")
-    ap.add_argument("--launch-idle", action="store_true",
-                    help="KFAC.launch_policy = 'idle' (launch when the stream drains)")
-    ap.add_argument("--partition", type=int, default=0,
-                    help="CUs reserved for the overlapped inversion (KFAC.partition_cus; 0 = none)")
     ap.add_argument("--single-buffer", action="store_true",
                     help="KFAC.double_buffer = False (the data stream waits for each "
                          "inversion to have read its factors)")
@@ -281,8 +275,7 @@ def main(argv=None):
     device = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
-    # all GPU work on one non-default stream (the legacy default stream would
-    # serialise with the CU-masked streams of --partition)
+    # all GPU work on one non-default stream
     torch.cuda.set_stream(torch.cuda.Stream(device))
 
     from bnn_kfac_amd import _native as N
@@ -293,13 +286,13 @@ def main(argv=None):
     net = build_model(args.config, device)
     layers = [m for m in net.modules() if isinstance(m, (torch.nn.Linear, torch.nn.Conv2d))]
     kfac = DistributedKFAC(net) if world > 1 else KFAC(net)
-    kfac.partition_cus = args.partition
+    # pipelined passes: the pivot verdict of inversion k is read at the next
+    # invert() / inv_state read instead of inside invert() (the library's default,
+    # the reference's behaviour), so pass k+1 is queued behind inversion k and
+    # overlaps it; every verdict is still read inside the timed region below
+    kfac.eager_verdict = False
     if args.launch_first:
         kfac.launch_first = args.launch_first
-    if args.launch_idle:
-        kfac.launch_policy = "idle"
-    if args.async_invert:
-        kfac.async_invert = True
     if args.single_buffer:
         kfac.double_buffer = False
     recs = synthetic_records(specs, images, device, seed=1234 + rank)
@@ -466,8 +459,7 @@ def main(argv=None):
                           "baseline_config": cfg, "global_batch": batch * world,
                           "images_per_rank": images, "parallelism": f"dp{world}",
                           "inversion": ("sharded" if getattr(kfac, "_sharded_last", False)
-                                        else "replicated"),
-                          "inversion_cus": args.partition or "shared"},
+                                        else "replicated")},
                "roofline": roofline, "cpu_baseline": cpu, "breakdown": breakdown,
                "allreduce_ms_per_step": allreduce_ms,
                "serial_images_per_s": serial, "e2e_images_per_s": e2e}

@@ -7,7 +7,6 @@ on the tensor's device, passed to every call explicitly.
 """
 from __future__ import annotations
 
-import atexit
 import ctypes
 import os
 import threading
@@ -99,15 +98,8 @@ SIGNATURES = {
     "kfac_sample_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(SampleJob), ctypes.c_int]),
     "kfac_sample": (ctypes.c_int, [ctypes.POINTER(SampleJob), ctypes.c_int, ctypes.c_int, c_vp,
                                    ctypes.c_size_t, c_vp]),
-    "kfac_invert_phase": (ctypes.c_int, [ctypes.POINTER(InvertJob), ctypes.c_int, c_vp, ctypes.c_size_t,
-                                         c_vp, ctypes.c_int, c_vp]),
     "kfac_tri_pack": (ctypes.c_int, [ctypes.POINTER(TriJob), ctypes.c_int, c_vp, c_vp]),
     "kfac_tri_unpack": (ctypes.c_int, [ctypes.POINTER(TriJob), ctypes.c_int, c_vp, ctypes.c_int, c_vp]),
-    "kfac_cu_count": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
-    "kfac_set_cu_budget": (ctypes.c_int, [ctypes.c_int]),
-    "kfac_stream_create_cu_mask": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
-                                                  ctypes.POINTER(c_vp)]),
-    "kfac_stream_destroy": (ctypes.c_int, [c_vp]),
     "kfac_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "kfac_profile_read": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_int64)]),
@@ -245,21 +237,6 @@ def invert(jobs, device: torch.device, inputs_read=None) -> torch.Tensor:
     return info
 
 
-def invert_prepare(jobs, device: torch.device, stream: int):
-    """(job array, workspace, device info tensor) for kfac_invert_phase on `stream`."""
-    arr = as_array(InvertJob, jobs)
-    need = lib().kfac_invert_workspace_bytes(arr, len(jobs))
-    ws = workspace.get(device, need, stream)
-    info = torch.empty(len(jobs), dtype=torch.int32, device=device)
-    return arr, ws, info
-
-
-def invert_phase(arr, ws: torch.Tensor, info: torch.Tensor, phase: int, stream: int) -> None:
-    """kfac_invert_phase (ctypes releases the GIL for the call: safe from a worker thread)."""
-    check(lib().kfac_invert_phase(arr, len(arr), ws.data_ptr(), ws.numel(), info.data_ptr(), phase, stream),
-          "kfac_invert_phase")
-
-
 def tri_jobs(factors):
     """[TriJob] of square row-major factors laid out back to back in a packed
     lower-triangle buffer, and that buffer's length (elements)."""
@@ -284,51 +261,6 @@ def tri_unpack(jobs, packed: torch.Tensor, mode: int) -> None:
     """kfac_tri_unpack (TRI_SYMMETRIC mirrors, TRI_LOWER zeroes the upper triangle)."""
     check(lib().kfac_tri_unpack(as_array(TriJob, jobs), len(jobs), packed.data_ptr(), int(mode),
                                 stream_handle(packed.device)), "kfac_tri_unpack")
-
-
-def cu_count(device: torch.device) -> int:
-    n = ctypes.c_int()
-    check(lib().kfac_cu_count(device.index if device.index is not None else 0, ctypes.byref(n)),
-          "kfac_cu_count")
-    return n.value
-
-
-def set_cu_budget(cus: int) -> None:
-    """CUs the factor launches are planned for (kfac_set_cu_budget; 0 = all)."""
-    check(lib().kfac_set_cu_budget(int(cus)), "kfac_set_cu_budget")
-
-
-def cu_mask_stream(device: torch.device, cus) -> "torch.cuda.ExternalStream":
-    """A stream confined to the CUs in `cus` (kfac_stream_create_cu_mask), as a torch
-    ExternalStream (the library keeps it for the process lifetime)."""
-    words = (max(cus) // 32 + 1) if cus else 1
-    mask = (ctypes.c_uint32 * words)()
-    for c in cus:
-        mask[c // 32] |= 1 << (c % 32)
-    handle = c_vp()
-    with torch.cuda.device(device):
-        check(lib().kfac_stream_create_cu_mask(mask, words, ctypes.byref(handle)),
-              "kfac_stream_create_cu_mask")
-    if not _mask_streams:
-        atexit.register(_destroy_mask_streams)
-    _mask_streams.append((device, handle.value))
-    return torch.cuda.ExternalStream(handle.value, device=device)
-
-
-_mask_streams = []
-
-
-def _destroy_mask_streams():
-    """Drain and destroy the CU-masked streams before the HIP runtime tears down
-    (left to the runtime's own teardown, it crashed under rocprofv3)."""
-    while _mask_streams:
-        device, handle = _mask_streams.pop()
-        try:
-            torch.cuda.synchronize(device)
-            lib().kfac_stream_destroy(c_vp(handle))
-        except Exception:  # interpreter shutdown: best effort
-            pass
-
 
 
 def syev(jobs, device: torch.device) -> torch.Tensor:

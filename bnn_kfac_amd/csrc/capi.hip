@@ -99,25 +99,3 @@ extern "C" int kfac_profile_reset(void) {
   g_done.clear();
   return KFAC_OK;
 }
-
-// ---------------------------------------------------------------- CU partitions
-extern "C" int kfac_cu_count(int device, int* count) {
-  if (!count) return KFAC_EINVAL;
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return KFAC_ELAUNCH;
-  *count = prop.multiProcessorCount;
-  return KFAC_OK;
-}
-
-extern "C" int kfac_stream_create_cu_mask(const uint32_t* mask, int words, void** stream) {
-  if (!mask || words <= 0 || !stream) return KFAC_EINVAL;
-  hipStream_t s = nullptr;
-  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask) != hipSuccess) return KFAC_ELAUNCH;
-  *stream = (void*)s;
-  return KFAC_OK;
-}
-
-extern "C" int kfac_stream_destroy(void* stream) {
-  if (!stream) return KFAC_EINVAL;
-  return hipStreamDestroy((hipStream_t)stream) == hipSuccess ? KFAC_OK : KFAC_ELAUNCH;
-}

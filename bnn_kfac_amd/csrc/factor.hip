@@ -284,13 +284,11 @@ __device__ __forceinline__ void factor_task_narrow_direct(const FactorJobDev& J,
   store_narrow(J, J.slab + (size_t)split * TILE * TILE, acc, lds);
 }
 
-// NSLOT ring slots (2: one stage in flight, 4 WGs/CU; 3: two in flight, 3 WGs/CU);
-// NACC independent accumulators per wave (k-steps interleaved) to keep back-to-back
-// MFMAs off the 64-cycle dependent-accumulator latency.
-template <int GBK, int NSLOT, int NACC, int MODE = 0, int SUB = 1>
+// NSLOT ring slots (2: one stage in flight, 4 WGs/CU); one barrier per stage.
+template <int GBK, int NSLOT>
 __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, const float* const* segs,
                                                  int local, float* lds, int split_major) {
-  static_assert(NSLOT >= 2 * SUB, "ring must hold the computed step and the next one");
+  static_assert(NSLOT >= 2, "ring must hold the computed stage and the next one");
   // split-major order: xcd_task hands every XCD a contiguous range of K-splits of
   // ALL tiles, so each XCD streams ~1/8 of the operand rows through its L2 once
   // (tile-major gave every XCD all K of its tiles' panels: ~8x the HBM fetch on
@@ -306,36 +304,32 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, const fl
   // quadrant of this wave, rotated per dispatch round: the ~4 workgroups sharing a CU
   // put their idle quadrants (strictly-upper on diagonal tiles, tile padding) on
   // different SIMDs instead of all on the same one
-  const int qw = (MODE & 128) ? wave : (wave + (int)(blockIdx.x >> 8)) & 3;
+  const int qw = (wave + (int)(blockIdx.x >> 8)) & 3;
   const int qi = qw >> 1, qj = qw & 1;
   const bool same = ti == tj;
   const bool active = !(same && qi < qj) && ti * TILE + qi * 32 < J.n && tj * TILE + qj * 32 < J.n;
   const bool narrow = J.n <= 32;  // one 32x32 quadrant: the 4 waves split K instead
-  floatx16 acc[NACC];
+  floatx16 acc;
 #pragma unroll
-  for (int c = 0; c < NACC; ++c)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) acc[c][v] = 0.f;
+  for (int v = 0; v < 16; ++v) acc[v] = 0.f;
 
   static_assert(GBK == BK, "a ring slot is one planner stage");
-  if (s1 > s0 && !(MODE & 64)) {
-    // ring of NSLOT slots of GBK rows; one barrier per step of SUB slots, so
-    // NSLOT - SUB slots are in flight while a step computes.  Slots are issued and
-    // landed in stage order, each walked by its own cursor across batch boundaries.
+  if (s1 > s0) {
+    // ring of NSLOT slots of GBK rows; NSLOT - 1 slots are in flight while a stage
+    // computes.  Slots are issued and landed in stage order, each walked by its own
+    // cursor across batch boundaries.
     constexpr int GSLOT = 2 * GBK * TILE;  // floats per ring slot (A and B panels)
     const int64_t rows = J.x.rows;
     GldsPanel<GBK> pa, pb;
     pa.init(J.x, ti * TILE, wave, lane, rows);
     pb.init(J.x, tj * TILE, wave, lane, rows);
     const int ns = (int)(s1 - s0);  // slots of this task
-    const int nstep = (ns + SUB - 1) / SUB;
     const int per = (same ? 1 : 2) * GldsPanel<GBK>::NCH;  // LDS-DMA instructions per slot per thread
     StageCursor ic, fc;  // next slot to issue / to land
     ic.init(J, s0);
     fc = ic;
     const float* ibase = seg_base(J, segs, ic.seg);
     auto issue = [&](int sl) {
-      if (MODE & 4) return;
       float* slot = lds + (sl % NSLOT) * GSLOT;
       pa.issue(ibase, ic.k, slot, wave);
       if (!same) pb.issue(ibase, ic.k, slot + GBK * TILE, wave);
@@ -344,146 +338,86 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, const fl
       if (ic.seg != seg && sl + 1 < ns) ibase = seg_base(J, segs, ic.seg);
     };
 #pragma unroll
-    for (int p0 = 0; p0 < NSLOT - SUB; ++p0)
+    for (int p0 = 0; p0 < NSLOT - 1; ++p0)
       if (p0 < ns) issue(p0);
     const int h = lane >> 5, rr = lane & 31;
-    for (int st = 0; st < nstep; ++st) {
-      // slots of step st landed; those issued after them may still fly
-      const int need = min(ns - 1, SUB * st + SUB - 1);
-      const int issued = min(ns - 1, SUB * st + NSLOT - SUB - 1);
-      vm_wait(per * (issued - need));
+    for (int st = 0; st < ns; ++st) {
+      // slot st landed; those issued after it may still fly
+      const int issued = min(ns - 1, st + NSLOT - 2);
+      vm_wait(per * (issued - st));
+      float* slot = lds + (st % NSLOT) * GSLOT;
+      pa.fixup(fc.k, slot);
+      if (!same) pb.fixup(fc.k, slot + GBK * TILE);
+      fc.next(rows);
+      stage_barrier();  // stage st visible to all waves; everyone is done with stage st-1's slot
+      if (st + NSLOT - 1 < ns) issue(st + NSLOT - 1);
+      if (narrow) {
+        const float* a = slot + h * TILE + rr;
 #pragma unroll
-      for (int u = 0; u < SUB; ++u) {
-        const int sl = SUB * st + u;
-        if (sl < ns) {
-          float* slot = lds + (sl % NSLOT) * GSLOT;
-          pa.fixup(fc.k, slot);
-          if (!same) pb.fixup(fc.k, slot + GBK * TILE);
-          fc.next(rows);
+        for (int s2 = 0; s2 < GBK / 8; ++s2) {
+          const int ks = 2 * (wave * (GBK / 8) + s2);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ks * TILE], a[ks * TILE], acc, 0, 0, 0);
         }
-      }
-      stage_barrier();  // step st visible to all waves; everyone is done with step st-1's slots
+      } else if (active) {
+        const float* a = slot + h * TILE + qi * 32 + rr;
+        const float* b = slot + (same ? 0 : GBK * TILE) + h * TILE + qj * 32 + rr;
+        float av[GBK / 2], bv[GBK / 2];
 #pragma unroll
-      for (int u = 0; u < SUB; ++u) {
-        const int sl = SUB * st + NSLOT - SUB + u;
-        if (sl < ns) issue(sl);
-      }
+        for (int s2 = 0; s2 < GBK / 2; ++s2) {
+          av[s2] = a[2 * s2 * TILE];
+          bv[s2] = b[2 * s2 * TILE];
+        }
 #pragma unroll
-      for (int u = 0; u < SUB; ++u) {
-        const int sl = SUB * st + u;
-        if (SUB > 1 && sl >= ns) break;
-        const float* slot = lds + (sl % NSLOT) * GSLOT;
-        if (narrow) {
-          const float* a = slot + h * TILE + rr;
+        for (int s2 = 0; s2 < GBK / 2; ++s2)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s2], bv[s2], acc, 0, 0, 0);
+        // DS reads interleaved with the MFMAs (-1.2 us of 42 on the MLP update; a deeper
+        // lookahead, the reads of MFMA pair t+2..4 issued with pair t, measured equal)
 #pragma unroll
-          for (int s2 = 0; s2 < GBK / 8; ++s2) {
-            const int ks = 2 * (wave * (GBK / 8) + s2);
-            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ks * TILE], a[ks * TILE], acc[0], 0, 0, 0);
-          }
-        } else if (active) {
-          const float* a = slot + h * TILE + qi * 32 + rr;
-          const float* b = slot + (same ? 0 : GBK * TILE) + h * TILE + qj * 32 + rr;
-          float av[GBK / 2], bv[GBK / 2];
-#pragma unroll
-          for (int s2 = 0; s2 < GBK / 2; ++s2) {
-            if (MODE & 16) {
-              av[s2] = (float)(lane + s2);
-              bv[s2] = (float)(lane - s2);
-            } else {
-              av[s2] = a[2 * s2 * TILE];
-              bv[s2] = b[2 * s2 * TILE];
-            }
-          }
-          if (MODE & 1) __builtin_amdgcn_s_setprio(1);
-          if (MODE & 8) {
-#pragma unroll
-            for (int s2 = 0; s2 < GBK / 2; ++s2) acc[0][s2 & 15] += av[s2] * bv[s2];
-          } else {
-#pragma unroll
-            for (int s2 = 0; s2 < GBK / 2; ++s2)
-              acc[s2 % NACC] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s2], bv[s2], acc[s2 % NACC], 0, 0, 0);
-          }
-          // (a deeper DS-read lookahead, the reads of MFMA pair t+2..4 issued with pair t,
-          // measured equal: 0.60 ms of tiles per MLP pass either way)
-          if (MODE & 2) {
-#pragma unroll
-            for (int s2 = 0; s2 < GBK / 2; ++s2) {
-              __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // 2 DS reads
-              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-            }
-          }
-          if (MODE & 1) __builtin_amdgcn_s_setprio(0);
+        for (int s2 = 0; s2 < GBK / 2; ++s2) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // 2 DS reads
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
         }
       }
     }
   }
   if (narrow) {  // (narrow => one tile, diagonal: A and B panels are the same)
     __syncthreads();
-    store_narrow(J, J.slab + ((size_t)tile * J.splits + split) * TILE * TILE, acc[0], lds);
+    store_narrow(J, J.slab + ((size_t)tile * J.splits + split) * TILE * TILE, acc, lds);
     return;
   }
   if (!active) return;
   float* out = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE + qi * 32 * TILE + qj * 32;
-#pragma unroll
-  for (int c = 1; c < NACC; ++c)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) acc[0][v] += acc[c][v];
-  put_partial(J, acc[0], [&](int v) { return &out[acc_row(v, lane) * TILE + (lane & 31)]; });
+  put_partial(J, acc, [&](int v) { return &out[acc_row(v, lane) * TILE + (lane & 31)]; });
 }
 
 
 // One launch per grouped update.  The row-major family (FAMILY = KFAC_ROWMAJOR)
 // takes the LDS-DMA path when a job's operand allows it, else the register-staged
 // row-major path; channel-major and im2col jobs get launches (and register budgets)
-// of their own, instantiated per layout.
-// MODE & 512 (microbenchmarks only): per-workgroup start / end s_memrealtime stamps
-__device__ unsigned long long g_syrk_stamps[2 * 16384];
-__device__ unsigned g_syrk_hw[2 * 16384];  // HW_ID, XCC_ID of the workgroup
-
-template <int GBK, int NSLOT, int MODE = 0, int SUB = 1, int FAMILY = KFAC_ROWMAJOR>
+// of their own, instantiated per layout.  GLDS_ONLY: every job takes the LDS-DMA
+// path (or the narrow direct-load path), and the ring is all the LDS (32 KB, not the
+// register-staged path's 34 KB): 4 resident workgroups leave 32 KB of a CU's 160,
+// room for a 32-tile inversion workgroup (29 KB) of an overlapped invert().
+template <int GBK, int NSLOT, bool GLDS_ONLY = false, int FAMILY = KFAC_ROWMAJOR>
 __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs args) {
   constexpr int RING = FAMILY == KFAC_ROWMAJOR ? NSLOT * 2 * GBK * TILE : 0;
-  // MODE & 256: every job takes the LDS-DMA path, the ring is all the LDS (32 KB, not
-  // the register-staged path's 34 KB): 4 resident workgroups leave 32 KB of a CU's
-  // 160, room for a 32-tile inversion workgroup (29 KB) of an overlapped invert()
-  constexpr int LDSF = (MODE & 256) ? RING : ((4 * PANEL > RING) ? 4 * PANEL : RING);
+  constexpr int LDSF = GLDS_ONLY ? RING : ((4 * PANEL > RING) ? 4 * PANEL : RING);
   __shared__ __attribute__((aligned(16))) float lds[LDSF];
   // Workgroups of later dispatch rounds (blockIdx / 256: the ~4 sharing a CU) start a
   // fraction of a stage later, so their DMA waits and barriers interleave instead of
   // stalling all 16 waves of a CU together (measured +2.5% on the MLP update).
-  if (!(MODE & 32))
-    for (int i = 0; i < args.stagger * (int)(blockIdx.x >> 8); ++i) __builtin_amdgcn_s_sleep(8);
+  for (int i = 0; i < args.stagger * (int)(blockIdx.x >> 8); ++i) __builtin_amdgcn_s_sleep(8);
   const int task = xcd_task(blockIdx.x, gridDim.x);
   int j = 0;
   while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
   const FactorJobDev& J = args.job[j];
   const int local = task - J.task_begin;
-  if constexpr ((MODE & 512) != 0) {
-    if (threadIdx.x == 0 && blockIdx.x < 16384) {
-      g_syrk_stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-      g_syrk_hw[2 * blockIdx.x] = __builtin_amdgcn_s_getreg(4 | (31 << 11));       // HW_REG_HW_ID
-      g_syrk_hw[2 * blockIdx.x + 1] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
-    }
-  }
-  struct StampEnd {
-    __device__ ~StampEnd() {
-      if constexpr ((MODE & 512) != 0) {
-        __syncthreads();
-        if (threadIdx.x == 0 && blockIdx.x < 16384)
-          g_syrk_stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-      }
-    }
-  } stamp_end;
   if constexpr (FAMILY == KFAC_ROWMAJOR) {
     const float* const* segs = args.segs;
-    if constexpr ((MODE & 256) != 0) {
-      if (J.glds)
-        factor_task_glds<GBK, NSLOT, 1, MODE, SUB>(J, segs, local, lds, args.split_major);
-      else
-        factor_task_narrow_direct(J, segs, local, lds);
-    }
-    else if (J.glds)
-      factor_task_glds<GBK, NSLOT, 1, MODE, SUB>(J, segs, local, lds, args.split_major);
+    if (J.glds)
+      factor_task_glds<GBK, NSLOT>(J, segs, local, lds, args.split_major);
+    else if constexpr (GLDS_ONLY)
+      factor_task_narrow_direct(J, segs, local, lds);
     else
       factor_task<KFAC_ROWMAJOR>(J, segs, local, lds);
   } else {
@@ -491,12 +425,11 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
   }
 }
 
-// production configuration: 32-row stages, 2-slot ring (one stage in flight),
-// DS reads interleaved with the MFMAs (MODE 2: -1.2 us of 42 on the MLP update)
-#define kfac_factor_tiles kfac_factor_tiles_t<32, 2, 2>
-#define kfac_factor_tiles_glds kfac_factor_tiles_t<32, 2, 2 | 256>
-#define kfac_factor_tiles_channel kfac_factor_tiles_t<32, 2, 2, 1, KFAC_CHANNEL>
-#define kfac_factor_tiles_patch kfac_factor_tiles_t<32, 2, 2, 1, KFAC_PATCH>
+// production configuration: 32-row stages, 2-slot ring (one stage in flight)
+#define kfac_factor_tiles kfac_factor_tiles_t<32, 2>
+#define kfac_factor_tiles_glds kfac_factor_tiles_t<32, 2, true>
+#define kfac_factor_tiles_channel kfac_factor_tiles_t<32, 2, false, KFAC_CHANNEL>
+#define kfac_factor_tiles_patch kfac_factor_tiles_t<32, 2, false, KFAC_PATCH>
 
 // ------------------------------------------------------------ conv operands
 // Conv2d factors with each image staged whole in LDS (replaces the per-element
@@ -548,15 +481,6 @@ struct ConvGeom {
 template <int LAYOUT, int PMAXE, bool STRIDE1, int CB = CONV_CB>
 __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args, ConvGeom cg) {
   extern __shared__ __attribute__((aligned(16))) float cimg[];
-#ifdef KFAC_CONV_STAMPS  // microbenchmarks only: per-workgroup start / end stamps
-  if (threadIdx.x == 0 && blockIdx.x < 16384) g_syrk_stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-  struct StampEnd {
-    __device__ ~StampEnd() {
-      if (threadIdx.x == 0 && blockIdx.x < 16384)
-        g_syrk_stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-    }
-  } stamp_end;
-#endif
   const int task = xcd_task(blockIdx.x, gridDim.x);
   int jx = 0;
   while (jx + 1 < args.njobs && task >= args.task_end[jx]) ++jx;
@@ -1072,10 +996,6 @@ static int64_t job_stages(const kfac_factor_job& j) { return job_sps(j) * job_ns
 // A job with a deferred-reduction accumulator keeps the accumulator's split count
 // (its layout): its stage range is cut into that many equal chunks (trailing splits
 // of a smaller batch may be empty and then contribute zero).
-// CUs the SYRK launches may occupy (kfac_set_cu_budget): 0 = all 256.  Set when
-// part of the chip is reserved (a CU-masked inversion stream running beside them).
-static int g_cu_budget = 0;
-
 // Row-major operand with 16-byte-aligned rows: the LDS-DMA paths.
 static bool job_glds(const kfac_factor_job& jb) {
   return jb.x.layout == KFAC_ROWMAJOR && jb.x.rows > 0 && jb.x.cols >= 4 && (jb.x.cols % 4) == 0 &&
@@ -1085,7 +1005,7 @@ static bool job_glds(const kfac_factor_job& jb) {
 static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
                       int64_t slots = 0) {
   // resident workgroups per CU: 4 (32 KB of LDS each)
-  if (slots <= 0) slots = 4 * (int64_t)(g_cu_budget > 0 ? g_cu_budget : 256);
+  if (slots <= 0) slots = 4 * 256;
   constexpr int64_t MIN_CHUNK = 8, OVERHEAD = 4;  // stages; ~per-task fixed cost in stages
   int64_t max_steps = 1;
   for (int i = 0; i < njobs; ++i) max_steps = std::max(max_steps, job_stages(jobs[i]));
@@ -1339,12 +1259,6 @@ static void launch_groups(const kfac_factor_job* jobs, int njobs, std::vector<kf
       sorted.push_back(jobs[i]);
       order.push_back(i);
     }
-}
-
-extern "C" int kfac_set_cu_budget(int cus) {
-  if (cus < 0 || cus > 4096) return KFAC_EINVAL;
-  g_cu_budget = cus;
-  return KFAC_OK;
 }
 
 extern "C" size_t kfac_factor_workspace_bytes(const kfac_factor_job* jobs, int njobs) {

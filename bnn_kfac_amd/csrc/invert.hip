@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <vector>
 
 #include "kfac_common.h"
 
@@ -106,16 +107,6 @@ static int invert_phase(const kfac_invert_job* jobs, int njobs, void* workspace,
     for (int i = g; i < g + ng; ++i) ws += job_ws(jobs[i], small);
   }
   return KFAC_OK;
-}
-
-extern "C" int kfac_invert_phase(const kfac_invert_job* jobs, int njobs, void* workspace,
-                                 size_t workspace_bytes, int32_t* info, int phase, kfac_stream_t stream) {
-  const int rc = check_jobs(jobs, njobs);
-  if (rc) return rc;
-  if (phase != 0 && phase != 1) return KFAC_EINVAL;
-  if (workspace_bytes < kfac_invert_workspace_bytes(jobs, njobs)) return KFAC_EWORKSPACE;
-  ProfScope ps(KFAC_PROF_INVERT, (hipStream_t)stream);
-  return invert_phase(jobs, njobs, workspace, info, (hipStream_t)stream, phase);
 }
 
 extern "C" int kfac_invert_ex(const kfac_invert_job* jobs, int njobs, void* workspace,

@@ -19,7 +19,7 @@ from __future__ import annotations
 
 import copy
 from abc import ABC, abstractmethod
-from typing import Any, List, Union
+from typing import Any, List, NamedTuple, Union
 
 import numpy as np
 import torch
@@ -147,6 +147,16 @@ class Curvature(ABC):
         print('Loading %s complete!\n' % filename)
 
 
+class _Pending(NamedTuple):
+    """An inversion whose pivot verdict is not read yet."""
+    done: Any            # torch.cuda.Event after the verdict's copy to `host`
+    host: Tensor         # pinned int32, one per job (0 = positive definite)
+    layers: list         # layers of the inversion, two jobs (A, G) each
+    target: dict         # the inv_state dict the layers' factors went into
+    outs: list           # the L factors (kept alive until ordered after)
+    on_side: bool        # issued on a side stream (the caller's stream must wait)
+
+
 class KFAC(Curvature):
     r"""Kronecker-factored Fisher (models/curvatures.py:277-405) on MI355X.
 
@@ -211,7 +221,6 @@ class KFAC(Curvature):
         # pass-then-invert loop the reference's scripts run (the host's issue of the
         # pass is no longer overlapped): kept at 1.
         self.launch_first = 1    # (property: also restarts the doubling)
-        self.launch_policy = "double"
         self._fast = None        # job templates of the last slow-path update (see _remember)
         self._acc_buf = None     # device buffer of the accumulators
         self._acc_map = None     # F pointer -> (acc pointer, splits) of the pending cycle
@@ -220,42 +229,18 @@ class KFAC(Curvature):
         self._acc_device = None
         self._info_pool = []     # free pinned int32 readback buffers of the pivot checks
         self._inv_older = []     # earlier inversions whose verdict is not read yet (in order)
-        self._inv_pending = None  # (event, host info, layers, inv_state dict, outputs, on side
-                                  # stream) until settled
+        self._inv_pending = None  # _Pending of the last inversion until its verdict is settled
         self.overlap_invert = True  # invert() on a side stream (see invert)
-        # eager_verdict (opt-in): invert() waits for its own pivot check and raises
-        # LinAlgError itself, as the reference's invert does (curvatures.py:393-396);
-        # by default the verdict is settled at the next inv_state read or invert(), so
-        # the next data pass can be queued behind the inversion without a host sync
-        self.eager_verdict = False
-        # opt-in with overlap_invert: the inversion's step launches (phase 1 of
-        # kfac_invert_phase) issued by a worker thread.  Off by default since the
-        # merged step chain replays from a hipGraph (one call): the worker then saved
-        # no host time and its GIL hand-offs made the host's issue time jittery
-        # (MLP line 0.52-0.64 ms of host per step with it, 0.52-0.53 without)
-        self.async_invert = False
-        self._inv_exec = None
-        self._inv_streams = {}    # device index -> side stream
-        # CU partition (opt-in; overlap_invert only; 0 = none): the inversion stream is
-        # confined to `partition_cus` CUs (a multiple of 8: that many / 8 per XCD), and
-        # a data pass that starts while that inversion may still run is launched on a
-        # stream confined to the other CUs, its SYRK planned for them (_cycle_setup).
-        # Without it the pass's one-wave SYRK launches hold every CU's LDS and the
-        # inversion's launches wait for them to drain.  Used only when the caller works
-        # on a non-default stream: CU-masked streams are blocking streams, so with the
-        # legacy default stream every event between them serialises (measured: 2x
-        # slower per pass instead of faster).
-        self.partition_cus = 0
-        self._part = {}           # device index -> (data stream, inversion stream, data CUs) | False
-        self._cycle_stream = None  # data stream of the pending cycle (None: the caller's stream)
-        self._cycle_hold = []      # (event on it, records its launches read) until they ran
+        # eager_verdict (default, the reference's behaviour): invert() waits for its own
+        # pivot check and raises LinAlgError itself, as the reference's invert does
+        # (curvatures.py:393-396).  False (opt-in, bench.py): the verdict is settled at
+        # the next inv_state read or invert(), so the next data pass is queued behind
+        # the inversion without a host sync and overlaps it.
+        self.eager_verdict = True
+        self._inv_streams = {}    # device index -> side streams
 
     def reset(self):
         """Forget the accumulated factors (start a new data pass); device buffers are kept."""
-        if getattr(self, "_cycle_stream", None) is not None:  # a dropped cycle: keep later work behind it
-            torch.cuda.current_stream(self._acc_device).wait_stream(self._cycle_stream)
-            self._cycle_stream = None
-            self._cycle_hold = []
         self._queue = []
         self._queue_bytes = 0
         self._launch_at = self.launch_first
@@ -294,76 +279,10 @@ class KFAC(Curvature):
             self._await_readers()
 
     def _end_cycle(self, jobs):
-        """Reduce the cycle's accumulators into the factors; the caller's stream then
-        waits for the cycle's stream (every later reader of `state` is behind it)."""
-        device = self._acc_device
-
-        def reduce():
-            self._await_readers()  # (on the stream the reduce is issued on)
-            N.factor_flush(jobs, device)
-        self._on_cycle_stream(device, reduce)
-        ds, self._cycle_stream = self._cycle_stream, None
-        if ds is not None:
-            torch.cuda.current_stream(device).wait_stream(ds)
-        self._cycle_hold = []
-
-    def _partition(self, device):
-        """(data stream, inversion stream, data CUs) of the CU partition, or None."""
-        if device.type != "cuda" or not (self.overlap_invert and self.partition_cus > 0):
-            return None
-        if torch.cuda.current_stream(device).cuda_stream == 0:  # legacy default stream
-            return None
-        part = self._part.get(device.index)
-        if part is None:
-            ncu, k = N.cu_count(device), int(self.partition_cus)
-            part = False
-            if ncu >= 2 * k:
-                # mask bit i: CU i // 8 of XCD i % 8, so CUs 0..k-1 are k/8 per XCD
-                part = (N.cu_mask_stream(device, list(range(k, ncu))),
-                        N.cu_mask_stream(device, list(range(k))), ncu - k)
-            self._part[device.index] = part
-        return part or None
-
-    def _cycle_setup(self, device):
-        """Choose the stream (and CU budget) of a new accumulation cycle: the partition's
-        data stream while the previous inversion may still run on its CUs, else the
-        caller's stream and the whole chip."""
-        part = self._partition(device)
-        pend = self._joined(self._inv_pending) if part is not None else None
-        busy = (part is not None and pend is not None and pend[6] and not pend[0].query())
-        self._cycle_stream = part[0] if busy else None
-        if part is not None:
-            N.set_cu_budget(part[2] if busy else 0)
-
-    def _on_cycle_stream(self, device, fn, keep=()):
-        """Run the launch(es) of `fn` on the cycle's stream, behind the caller's work.
-        The records it reads are held until an event behind the launch has completed
-        (or the caller's stream has waited for the cycle): their memory, owned by the
-        caller's stream, is not reused under the launch.  (No record_stream: the
-        allocator's events on a CU-masked stream crashed interpreter teardown under
-        rocprofv3.)  The buffers the launches write (`_packed`, the accumulators) are
-        replaced only at a cycle start, after the caller's stream waited for the last."""
-        ds = self._cycle_stream
-        pend = self._joined(self._inv_pending) if ds is not None else None
-        if ds is not None and (pend is None or pend[0].query()):
-            # the inversion has finished: the rest of the cycle runs on the caller's
-            # stream over the whole chip (a long pass keeps only its first launches
-            # on the data CUs; the K-splits stay as planned)
-            cur = torch.cuda.current_stream(device)
-            cur.wait_stream(ds)
-            self._cycle_stream, self._cycle_hold, ds = None, [], None
-        if ds is None:
-            return fn()
-        ds.wait_stream(torch.cuda.current_stream(device))
-        with torch.cuda.stream(ds):
-            fn()
-        hold = self._cycle_hold
-        while hold and hold[0][0].query():
-            hold.pop(0)
-        if keep:
-            ev = torch.cuda.Event()
-            ev.record(ds)
-            hold.append((ev, list(keep)))
+        """Reduce the cycle's accumulators into the factors (one launch, on the
+        caller's stream, after any inversion still reading the target buffer)."""
+        self._await_readers()
+        N.factor_flush(jobs, self._acc_device)
 
     # curvatures.py:319-323
     def _save_input(self, module, input):
@@ -567,30 +486,15 @@ class KFAC(Curvature):
         fast = self._fast
         self._queue_bytes += (self._fast_bytes if fast is not None and entry[0] is fast[2]
                               else sum(t.numel() * t.element_size() for t in entry[2]))
-        # launch policy (the records held are capped by defer_bytes either way):
-        # * "double" (default): launch sizes double from `launch_first` up to
-        #   defer_batches -- a function of the update count only, so the launches'
-        #   K-splits, and with them the factors' fp32 summation order, are the same
-        #   on every run;
-        # * "idle": launch as soon as the caller's stream has drained, else keep
-        #   queueing (a pipelined pass becomes one or two large launches, ~2 % more
-        #   images/s on the MLP bench), but the grouping then follows GPU timing and
-        #   the factors can differ in their last bits from run to run.
+        # launch sizes double from `launch_first` up to defer_batches (the records held
+        # are capped by defer_bytes): a function of the update count only, so the
+        # launches' K-splits, and with them the factors' fp32 summation order, are the
+        # same on every run
         if len(self._queue) >= max(1, self.defer_batches) or self._queue_bytes >= self.defer_bytes:
             self._launch_queue()
-        elif self.launch_policy == "idle":
-            if self._stream_idle(entry[4]):
-                self._launch_queue()
         elif len(self._queue) >= self._launch_at:
             self._launch_at *= 2
             self._launch_queue()
-
-    def _stream_idle(self, device):
-        """True when every launch on the caller's stream (and the cycle's) has run."""
-        if device.type != "cuda":  # (the host test double runs on the CPU)
-            return True
-        stream = self._cycle_stream or torch.cuda.current_stream(device)
-        return stream.query()
 
     def _launch_queue(self):
         """Launch the queued updates: consecutive updates with the same job templates
@@ -613,7 +517,6 @@ class KFAC(Curvature):
                 groups.append(queue[start:i])
                 start = i
         tables = []
-        kept = [t for e in queue for t in e[2]]
         for group in groups:
             tmpl = group[0][0]
             jobs = []
@@ -633,7 +536,7 @@ class KFAC(Curvature):
                             job.beta = 1.0  # later batches add to the first one's result
                         jobs.append(job)
             self._defer(jobs, device)
-            self._on_cycle_stream(device, lambda: N.factor_update(jobs, device), kept)
+            N.factor_update(jobs, device)
         # queued records are released here (the host segment tables were read by the
         # calls); the caching allocator orders any reuse of the records' memory after
         # the launches on this stream
@@ -648,7 +551,6 @@ class KFAC(Curvature):
             acc_jobs, self._acc_flush, self._acc_map = self._acc_flush, None, None
             self._end_cycle(acc_jobs)
         if self._acc_map is None:
-            self._cycle_setup(device)
             first = {}
             for j in jobs:
                 first.setdefault(j.F, j)
@@ -696,8 +598,7 @@ class KFAC(Curvature):
         """L = cholesky(inverse(sqrt(s) F + sqrt(n) I)) per factor (curvatures.py:367-398)."""
         state = self.state  # (one flush: `state` completes the deferred reduction)
         assert state, "State dict is empty. Did you call 'update' prior to this?"
-        # the previous inversion's verdict is read later (no host wait here): its
-        # outputs are ordered before later work on the caller's stream now
+        # a previous inversion's verdict (deferred mode) is settled or queued here
         self._defer_verdict()
         if self._inv_state:
             Warning("State has already been inverted. Is this expected?")
@@ -714,19 +615,8 @@ class KFAC(Curvature):
         # stream waits only until the factors have been READ (kfac_invert_ex's
         # inputs_read event, after the first launch), so it may overwrite them.
         main = torch.cuda.current_stream(device)
-        # the CU partition only for latency-bound inversions (every factor within the
-        # one-launch-per-step range, <= 24 tiles of 64): a large factor's inversion is
-        # throughput-bound and needs the whole chip (wide MLP, 4097^2: 4x slower on 32 CUs)
-        part = self._partition(device) if self.overlap_invert else None
         latency_bound = max(F_.shape[0] for _, v in entries for F_ in v) <= 24 * 64
-        part_side = part is not None and latency_bound
-        side = ((part[1] if part_side else self._side_stream(device, alternate=latency_bound))
-                if self.overlap_invert else main)
-        if not latency_bound:
-            # same stream and workspace as the previous inversion: its worker-issued
-            # launches must be queued before this one's first launch overwrites it
-            for p in getattr(self, "_inv_older", []):
-                self._joined(p)
+        side = self._side_stream(device, alternate=latency_bound) if self.overlap_invert else main
         read = None
         if side is not main:
             side.wait_stream(main)
@@ -741,77 +631,30 @@ class KFAC(Curvature):
                     jobs.append(N.invert_job(F_, out, s ** 0.5, n ** 0.5))
                     pair.append(out)
                 outs.append((layer, tuple(pair)))
-            if read is not None and self.async_invert:
-                self._invert_async(device, main, side, part_side, jobs, outs, read, entries)
-                if self.eager_verdict:
-                    self._check_inverse()
-                return
             info = N.invert(jobs, device, inputs_read=read)
             # The pivot verdict travels back with a non-blocking copy into pinned
-            # memory; it is settled (event wait) at the next read of `inv_state` or the
-            # next invert(), so a data pass can be queued behind this inversion without
-            # a host sync in between.
-            pool = self._info_pool
-            while pool and pool[-1].numel() != info.numel():
-                pool.pop()
-            host = pool.pop() if pool else torch.empty(info.numel(), dtype=info.dtype, pin_memory=True)
+            # memory, on the side stream; eager_verdict waits for it right here,
+            # otherwise it is settled at the next read of `inv_state` or the next
+            # invert(), so a data pass can be queued behind this inversion.
+            host = self._pinned_info(info)
+            host.copy_(info, non_blocking=True)
             done = torch.cuda.Event()
             done.record(side)
-            # the copy goes on an ordinary torch stream: the pinned-memory allocator's
-            # stream bookkeeping must not name a CU-masked (library-owned) stream
-            cs = self._copy_stream(device) if part_side else side
-            if cs is not side:
-                cs.wait_event(done)
-            with torch.cuda.stream(cs):
-                host.copy_(info, non_blocking=True)
-            if cs is not side:
-                done = torch.cuda.Event()
-                done.record(cs)
         if read is not None:
             self._release(main, read, entries)
         for layer, pair in outs:
             self._inv_state[layer] = pair
-        self._inv_pending = (done, host, [layer for layer, _ in outs], self._inv_state,
-                             [t for _, pair in outs for t in pair], side is not main, part_side, None)
+        self._inv_pending = _Pending(done, host, [layer for layer, _ in outs], self._inv_state,
+                                     [t for _, pair in outs for t in pair], side is not main)
         if self.eager_verdict:
             self._check_inverse()
 
-    def _invert_async(self, device, main, side, part_side, jobs, outs, read, entries):
-        """invert() with overlap_invert: phase 0 (the launches that read F) here, the
-        caller's stream released behind it, phase 1 + the verdict readback from the
-        worker thread (every later use of the pending inversion joins it first)."""
-        sh = side.cuda_stream
-        arr, ws, info = N.invert_prepare(jobs, device, sh)
-        N.invert_phase(arr, ws, info, 0, sh)
-        read.record(side)
-        self._release(main, read, entries)
+    def _pinned_info(self, info):
+        """A pinned host int32 buffer for a verdict readback (pooled)."""
         pool = self._info_pool
         while pool and pool[-1].numel() != info.numel():
             pool.pop()
-        host = pool.pop() if pool else torch.empty(info.numel(), dtype=info.dtype, pin_memory=True)
-        done = torch.cuda.Event()
-        cs = self._copy_stream(device) if part_side else side
-
-        def rest():
-            with torch.cuda.device(device):
-                N.invert_phase(arr, ws, info, 1, sh)
-                if cs is not side:
-                    ev = torch.cuda.Event()
-                    ev.record(side)
-                    cs.wait_event(ev)
-                with torch.cuda.stream(cs):
-                    host.copy_(info, non_blocking=True)
-                done.record(cs)
-
-        if self._inv_exec is None:
-            import concurrent.futures
-            self._inv_exec = concurrent.futures.ThreadPoolExecutor(max_workers=1,
-                                                                   thread_name_prefix="kfac-invert")
-        fut = self._inv_exec.submit(rest)
-        for layer, pair in outs:
-            self._inv_state[layer] = pair
-        self._inv_pending = (done, host, [layer for layer, _ in outs], self._inv_state,
-                             [t for _, pair in outs for t in pair], True, part_side, fut)
+        return pool.pop() if pool else torch.empty(info.numel(), dtype=torch.int32, pin_memory=True)
 
     def _release(self, main, read, entries):
         """Let the caller's stream go past an inversion: straight away when the factors
@@ -824,21 +667,6 @@ class KFAC(Curvature):
                 self._buf_read[buf.data_ptr()] = read
                 return
         main.wait_event(read)
-
-    @staticmethod
-    def _joined(pending):
-        """The pending inversion with its worker-issued launches enqueued (re-raises
-        what they raised)."""
-        if pending is not None and pending[7] is not None:
-            pending[7].result()
-        return pending
-
-    def _copy_stream(self, device):
-        s = getattr(self, "_copy_streams", {}).get(device.index)
-        if s is None:
-            self._copy_streams = getattr(self, "_copy_streams", {})
-            s = self._copy_streams[device.index] = torch.cuda.Stream(device=device)
-        return s
 
     def _side_stream(self, device, alternate=True):
         """The side stream of this inversion: two high-priority streams taken in turn,
@@ -859,14 +687,14 @@ class KFAC(Curvature):
         self._inv_turn = getattr(self, "_inv_turn", 0) ^ 1
         return s[self._inv_turn]
 
-    def _order_after(self, pending):
+    @staticmethod
+    def _order_after(pending):
         """Later work on the caller's stream sees the inversion's factors, and the
         allocator keeps their memory until that work has run (no host wait)."""
-        done, _host, _layers, _target, outs, on_side, _, _ = self._joined(pending)
-        if on_side:
-            cur = torch.cuda.current_stream(outs[0].device)
-            cur.wait_event(done)
-            for t in outs:
+        if pending.on_side:
+            cur = torch.cuda.current_stream(pending.outs[0].device)
+            cur.wait_event(pending.done)
+            for t in pending.outs:
                 t.record_stream(cur)
 
     def _defer_verdict(self):
@@ -878,8 +706,7 @@ class KFAC(Curvature):
         if pending is not None:
             self._inv_pending = None
             self._inv_older.append(pending)
-        while self._inv_older and (len(self._inv_older) > 2 or
-                                   self._joined(self._inv_older[0])[0].query()):
+        while self._inv_older and (len(self._inv_older) > 2 or self._inv_older[0].done.query()):
             p = self._inv_older.pop(0)
             self._order_after(p)
             self._verdict(p)
@@ -903,17 +730,13 @@ class KFAC(Curvature):
 
     def _verdict(self, pending):
         """Wait for one inversion's pivot check and act on it."""
-        done, host, layers, target, outs, on_side, _, _ = self._joined(pending)
-        done.synchronize()
-        bad = host.numpy().copy()
-        self._info_pool.append(host)
-        if (bad < 0).any():
-            target.clear()
-            raise RuntimeError("kfac_invert: the inversion work queue timed out (no result)")
+        pending.done.synchronize()
+        bad = pending.host.numpy().copy()
+        self._info_pool.append(pending.host)
         if bad.any():
             first = int(np.flatnonzero(bad)[0]) // 2  # two jobs (A, G) per layer
-            for layer in layers[first:]:
-                target.pop(layer, None)
+            for layer in pending.layers[first:]:
+                pending.target.pop(layer, None)
             # the fp64 device factorisation fails exactly where numpy's fallback
             # would, so end the same way without a CPU path
             print("PyTorch Cholesky is singular. Using Numpy.")

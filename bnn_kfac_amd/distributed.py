@@ -31,7 +31,7 @@ import torch.distributed as dist
 from torch.nn import Module, Sequential
 
 from . import _native as N
-from .curvatures import KFAC
+from .curvatures import KFAC, _Pending
 
 SHARD_MIN_N = 1536  # largest factor above this: the inversion is throughput-bound
 
@@ -55,9 +55,11 @@ class DistributedKFAC(KFAC):
     `update(batch_size, global_batch_size=None)`: the per-batch mean is taken over
     the GLOBAL batch (default: world_size x the local rows, i.e. equal shards).
     Local contributions accumulate into a private packed buffer; `allreduce()`
-    (called by `invert()`, and by any read of `state`, if needed) sums it over
-    ranks into `state`.  Reading `state` is therefore a collective call while a
-    pass is pending: every rank must do it.
+    (called by `invert()`, or explicitly, on EVERY rank) sums it over ranks into
+    `state`.  Reading `state` never communicates: it holds the reduced factors of
+    the passes all-reduced so far (a read while this rank's pass is pending warns
+    that the pass is not in it yet), so a rank-local read (`if rank == 0:
+    torch.save(kfac.state)`, logging) cannot deadlock the other ranks.
 
     `shard_inversion`: "auto" (shard when world > 1 and some factor is larger than
     1536), True or False.
@@ -98,12 +100,21 @@ class DistributedKFAC(KFAC):
             self._state = reduced
         self._pending = True
 
-    def flush(self):
-        """KFAC.flush, then the pass's all-reduce if one is pending (so `state` holds
-        every rank's updates, like the single-device state)."""
-        super().flush()
+    @property
+    def state(self):
+        """The all-reduced factors (no collective here; see the class docstring)."""
         if getattr(self, "_pending", False):
-            self.allreduce()
+            import warnings
+            warnings.warn("DistributedKFAC.state read while this rank's pass is not all-reduced "
+                          "yet: it holds the passes reduced so far; call allreduce() (or "
+                          "invert()) on every rank first", RuntimeWarning, stacklevel=2)
+        self.flush()
+        return self._state
+
+    @state.setter
+    def state(self, value):
+        self.flush()
+        self._state = value
 
     def _collective(self):
         return self.world > 1 or self.always_reduce
@@ -119,7 +130,7 @@ class DistributedKFAC(KFAC):
         collective over the packed lower triangles of every factor."""
         if not self._pending:
             return
-        KFAC.flush(self)  # the rank-local factors are complete only after the deferred reduce
+        self.flush()  # the rank-local factors are complete only after the deferred reduce
         local = self._local_state
         if self._collective() and local:
             factors = [F for pair in local.values() for F in pair]
@@ -219,7 +230,7 @@ class DistributedKFAC(KFAC):
         layers = [layer for layer, _ in entries]
         for k, layer in enumerate(layers):
             self._inv_state[layer] = (outs[2 * k], outs[2 * k + 1])
-        self._inv_pending = (done, host, layers, self._inv_state, outs, False, False, None)
+        self._inv_pending = _Pending(done, host, layers, self._inv_state, outs, False)
 
     def _readback(self, info):
         """(event, pinned host copy) of a device verdict vector, copied without a

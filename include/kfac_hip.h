@@ -159,12 +159,6 @@ KFAC_API int kfac_invert(const kfac_invert_job* jobs, int njobs, void* workspace
  * kfac_invert.                                                               */
 KFAC_API int kfac_invert_ex(const kfac_invert_job* jobs, int njobs, void* workspace,
                    size_t workspace_bytes, int32_t* info, void* inputs_read, kfac_stream_t stream);
-/* kfac_invert_ex in two calls: phase 0 = the launches that read F (the caller may
- * record its own "inputs read" event after it), phase 1 = the rest, on the same
- * stream, possibly from another host thread (KFAC.invert issues phase 1 from a
- * worker thread so its ~25 step launches do not hold up the next data pass). */
-KFAC_API int kfac_invert_phase(const kfac_invert_job* jobs, int njobs, void* workspace,
-                               size_t workspace_bytes, int32_t* info, int phase, kfac_stream_t stream);
 /* Single-factor convenience: KFAC.invert for one factor. */
 KFAC_API int kfac_damped_inv_chol(const float* F, int n, int64_t ldF, double sqrt_s, double sqrt_n,
                          float* L, int64_t ldL, void* workspace, size_t workspace_bytes,
@@ -272,20 +266,6 @@ enum kfac_prof_id { KFAC_PROF_FACTOR_TILES = 0, KFAC_PROF_FACTOR_REDUCE = 1, KFA
 KFAC_API int kfac_profile_enable(int on);
 KFAC_API int kfac_profile_read(int id, double* total_ms, int64_t* launches);
 KFAC_API int kfac_profile_reset(void);
-
-/* ------------------------------------------------------------ CU partitions
- * Streams whose dispatches are confined to a subset of the device's CUs
- * (hipExtStreamCreateWithCUMask; bit i of mask word i/32 = CU i).  KFAC runs a
- * data pass's SYRK launches and the (latency-bound, one-workgroup critical path)
- * inversion of the previous pass on disjoint CU sets, so neither waits for the
- * other's workgroups to drain from a CU.  kfac_cu_count: the device's CUs.   */
-KFAC_API int kfac_cu_count(int device, int* count);
-/* CUs the factor (SYRK) launches are planned for: 4 resident workgroups per CU,
- * split-K sized to fill them in as few rounds as possible.  0 = the whole chip
- * (256).  Lower it when the launches run on a CU-masked stream.              */
-KFAC_API int kfac_set_cu_budget(int cus);
-KFAC_API int kfac_stream_create_cu_mask(const uint32_t* mask, int words, void** stream);
-KFAC_API int kfac_stream_destroy(void* stream);
 
 /* ------------------------------------------------------------------- misc */
 KFAC_API const char* kfac_strerror(int status);

@@ -56,10 +56,16 @@ def _worker(rank, world, port, result_q, scenario):
                 kfac.record[net[0]] = [torch.from_numpy(A1[sl]), torch.from_numpy(G1[sl])]
                 kfac.record[net[2]] = [torch.from_numpy(A2[sl]), torch.from_numpy(G2[sl])]
                 kfac.update(cut[1] - cut[0], global_batch_size=gb)
-            if scenario == "state_read":
-                kfac.state  # a state read completes the pass (collective on every rank)
-            else:
-                kfac.allreduce()
+                if scenario == "state_read" and rank == 0:
+                    # a rank-local read mid-pass (logging, rank-0 checkpoint): no
+                    # collective, so it cannot hang the other ranks; it warns that the
+                    # pending pass is not in the reduced state yet
+                    import warnings
+                    with warnings.catch_warnings(record=True) as w:
+                        warnings.simplefilter("always")
+                        assert kfac.state == {}
+                    assert any("not all-reduced" in str(x.message) for x in w)
+            kfac.allreduce()
         dist.all_reduce = orig
         out = [t.numpy().copy() for pair in kfac.state.values() for t in pair]
         inv = None

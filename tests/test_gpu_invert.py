@@ -110,12 +110,35 @@ def test_kfac_invert_mlp_golden(hip_device):
     np.testing.assert_allclose(LA1[-8:], g["LA1_tail"], rtol=1e-2, atol=2e-3)
 
 
-def test_singular_raises_linalgerror(hip_device):
+def test_singular_raises_linalgerror(hip_device, capsys):
+    """Under the defaults invert() itself raises LinAlgError on a non-SPD factor,
+    after the reference's printed message (curvatures.py:390-396), so a caller's
+    `try: kfac.invert(...) except LinAlgError` catches it; the failing layer is not
+    assigned; a later damped inversion runs."""
     from bnn_kfac_amd.curvatures import KFAC
     g = golden("g2_singular.npz")
     assert str(g["outcome"]) == "LinAlgError"
     net = nn.Sequential(nn.Linear(6, 4)).to(hip_device)
     kfac = KFAC(net)
+    assert kfac.eager_verdict
+    kfac.record[net[0]] = [_t(g["a"], hip_device), _t(g["g"], hip_device)]
+    kfac.update(2)
+    with pytest.raises(np.linalg.LinAlgError):
+        kfac.invert(0.0, 1.0)
+    assert "PyTorch Cholesky is singular. Using Numpy." in capsys.readouterr().out
+    assert net[0] not in kfac.inv_state
+    kfac.invert(1.0, 1.0)  # damped: positive definite, no raise
+    assert net[0] in kfac.inv_state
+
+
+def test_singular_deferred_verdict(hip_device):
+    """eager_verdict = False (the bench's pipelined mode): the verdict is read back
+    asynchronously and raises at the next inv_state read or invert()."""
+    from bnn_kfac_amd.curvatures import KFAC
+    g = golden("g2_singular.npz")
+    net = nn.Sequential(nn.Linear(6, 4)).to(hip_device)
+    kfac = KFAC(net)
+    kfac.eager_verdict = False
     kfac.record[net[0]] = [_t(g["a"], hip_device), _t(g["g"], hip_device)]
     kfac.update(2)
     kfac.invert(0.0, 1.0)  # the verdict is read back asynchronously ...
@@ -127,23 +150,6 @@ def test_singular_raises_linalgerror(hip_device):
     with pytest.raises(np.linalg.LinAlgError):
         kfac.invert(1.0, 1.0)  # ... so that invert() reads it and raises (and does not run)
     kfac.invert(1.0, 1.0)
-    assert net[0] in kfac.inv_state
-
-
-def test_singular_eager_verdict_raises_in_invert(hip_device):
-    """KFAC.eager_verdict: invert() itself raises, as the reference's does
-    (curvatures.py:393-396), and a later good inversion still runs."""
-    from bnn_kfac_amd.curvatures import KFAC
-    g = golden("g2_singular.npz")
-    net = nn.Sequential(nn.Linear(6, 4)).to(hip_device)
-    kfac = KFAC(net)
-    kfac.eager_verdict = True
-    kfac.record[net[0]] = [_t(g["a"], hip_device), _t(g["g"], hip_device)]
-    kfac.update(2)
-    with pytest.raises(np.linalg.LinAlgError):
-        kfac.invert(0.0, 1.0)
-    assert net[0] not in kfac._inv_state
-    kfac.invert(1.0, 1.0)  # damped: positive definite, no raise
     assert net[0] in kfac.inv_state
 
 
@@ -164,14 +170,14 @@ def test_invert_identity_property_wide(hip_device):
     assert np.abs(E - np.eye(n)).max() < 1e-3
 
 
-@pytest.mark.parametrize("reset,async_invert", [(True, False), (False, False), (True, True)])
-def test_overlapped_inversion_matches_serial(hip_device, reset, async_invert):
+@pytest.mark.parametrize("reset", [True, False])
+def test_overlapped_inversion_matches_serial(hip_device, reset):
     """invert() runs on the side stream and the next pass is queued right behind it
-    (the bench's pattern: nothing read in between, so pass k+1's SYRK overlaps
-    inversion k).  With reset() the passes alternate two packed buffers and pass
-    k+2's flush overwrites the buffer inversion k read; without it every flush adds
-    into the buffer the previous inversion is reading.  Every pass's L factors equal
-    the serial path's bit for bit."""
+    (the bench's pattern, deferred verdicts: nothing read in between, so pass k+1's
+    SYRK overlaps inversion k).  With reset() the passes alternate two packed buffers
+    and pass k+2's flush overwrites the buffer inversion k read; without it every
+    flush adds into the buffer the previous inversion is reading.  Every pass's L
+    factors equal the serial path's bit for bit."""
     from bnn_kfac_amd.curvatures import KFAC
     torch.manual_seed(0)
     net = nn.Sequential(nn.Linear(784, 128), nn.ReLU(), nn.Linear(128, 10)).to(hip_device)
@@ -185,8 +191,7 @@ def test_overlapped_inversion_matches_serial(hip_device, reset, async_invert):
     def run(overlap):
         kfac = KFAC(net)
         kfac.overlap_invert = overlap
-        kfac.async_invert = async_invert  # (opt-in worker thread for phase 1)
-        kfac.partition_cus = 0  # one stream layout: same SYRK splits as the serial path
+        kfac.eager_verdict = False
         kept = []
         for batches in passes:
             if reset:
@@ -214,81 +219,48 @@ def test_overlapped_inversion_matches_serial(hip_device, reset, async_invert):
     assert np.abs(L.T @ R @ L - np.eye(R.shape[0])).max() < 1e-3
 
 
-@pytest.mark.parametrize("wgs", ["1", "7", "32", "200"])
-def test_flow_inversion_equals_per_step_launches(hip_device, monkeypatch, wgs):
-    """inv_flow (one persistent dataflow launch for every elimination step, any number
-    of workgroups — one included) gives the per-step launches' factors bit for bit."""
-    from bnn_kfac_amd import _native as N
-    rng = np.random.default_rng(11)
-    sizes = (785, 128, 129, 10, 1536, 64, 65)
-    mats = [_t(_spd(n, rng, 1e4), hip_device) for n in sizes]
-
-    def run(flow):
-        monkeypatch.setenv("KFAC_INV_FLOW", flow)
-        monkeypatch.setenv("KFAC_INV_FLOW_WGS", wgs)
-        outs = [torch.empty_like(F) for F in mats]
-        info = N.invert([N.invert_job(F, o, 200 ** 0.5, 0.04 ** 0.5) for F, o in zip(mats, outs)],
-                        hip_device)
-        torch.cuda.synchronize()
-        assert not info.cpu().any()
-        return outs
-
-    ref, got = run("0"), run("1")
-    for n, a, b in zip(sizes, ref, got):
-        assert torch.equal(a, b), n
-    F = mats[0].cpu().numpy()
-    np.testing.assert_allclose(got[0].cpu().numpy(), O.invert_factor(F, 0.04, 200), rtol=1e-4,
-                               atol=1e-7 * float(got[0].abs().max()))
-
-
-def test_cu_partitioned_passes_match_serial(hip_device):
-    """overlap_invert with the CU partition (opt-in): a pass that starts while the
-    previous inversion runs is launched on the data CUs' stream with its SYRK planned
-    for them (other K-splits: fp32 sums within rounding of the serial path's), the
-    inversion on its own CUs; every pass's L satisfies L^T R L = I on its own factors."""
+def test_double_buffer_slow_inversion_race(hip_device):
+    """A slow (4097-sized, throughput-bound) inversion still reading packed buffer P
+    while later passes reduce into the buffers: update -> invert -> reset looped, plus
+    update-after-invert without reset, pipelined (deferred verdicts).  state and
+    inv_state equal the same run with double_buffer = False and no overlap."""
     from bnn_kfac_amd.curvatures import KFAC
     torch.manual_seed(0)
-    net = nn.Sequential(nn.Linear(784, 128), nn.ReLU(), nn.Linear(128, 10)).to(hip_device)
-    g = torch.Generator(device=hip_device).manual_seed(5)
-    passes = [[(torch.rand(4096, 784, device=hip_device, generator=g),
-                torch.randn(4096, 128, device=hip_device, generator=g),
-                torch.rand(4096, 128, device=hip_device, generator=g),
-                torch.randn(4096, 10, device=hip_device, generator=g)) for _ in range(4)]
-              for _ in range(4)]
+    net = nn.Sequential(nn.Linear(4096, 16)).to(hip_device)
+    gen = torch.Generator(device=hip_device).manual_seed(7)
+    batches = [(torch.rand(1024, 4096, device=hip_device, generator=gen),
+                torch.randn(1024, 16, device=hip_device, generator=gen)) for _ in range(8)]
+    plan = ["u", "u", "i", "r", "u", "i", "r", "u", "i", "u", "i", "r", "u", "u", "i"]
 
-    def run(overlap):
+    def run(fast):
         kfac = KFAC(net)
-        kfac.overlap_invert = overlap
-        kfac.partition_cus = 32
-        kfac.launch_first = 1  # launches during the pass (the partition's data stream)
-        states, invs, used = [], [], []
-        for batches in passes:
-            kfac.reset()
-            for a1, g1, a2, g2 in batches:
-                kfac.record[net[0]] = [a1, g1]
-                kfac.record[net[2]] = [a2, g2]
-                kfac.update(a1.shape[0])
-                used.append(kfac._cycle_stream is not None)
-            kfac.invert(0.04, 200)
-            states.append([t.clone() for pair in kfac.state.values() for t in pair])
-            invs.append(dict(kfac._inv_state))
+        kfac.double_buffer = fast
+        kfac.overlap_invert = fast
+        kfac.eager_verdict = False
+        out, k = [], 0
+        for op in plan:
+            if op == "u":
+                kfac.record[net[0]] = list(batches[k % len(batches)])
+                k += 1
+                kfac.update(1024)
+            elif op == "i":
+                kfac.invert(0.04, 200)
+                out.append(dict(kfac._inv_state))
+            else:
+                kfac.reset()
+        st = [t.clone() for pair in kfac.state.values() for t in pair]
         _ = kfac.inv_state
         torch.cuda.synchronize()
-        return ([[t.cpu().numpy() for t in st] for st in states],
-                [[t.cpu().numpy() for pair in d.values() for t in pair] for d in invs], any(used))
+        return ([[t.cpu().numpy() for pair in d.values() for t in pair] for d in out],
+                [t.cpu().numpy() for t in st])
 
-    s_state, s_inv, _ = run(False)
-    with torch.cuda.stream(torch.cuda.Stream(hip_device)):  # the partition needs a non-default stream
-        p_state, p_inv, used = run(True)
-    assert used, "no pass ran on the partition's data stream"
-    for want_pass, got_pass in zip(s_state, p_state):
-        for want, got in zip(want_pass, got_pass):
-            np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-6 * np.abs(want).max())
-    for st, inv in zip(p_state, p_inv):
-        for F, L in zip(st, inv):
-            R = O.damped_factor(F.astype(np.float64), 0.04, 200)
-            Ld = L.astype(np.float64)
-            assert np.abs(Ld.T @ R @ Ld - np.eye(R.shape[0])).max() < 1e-3
+    want_inv, want_state = run(False)
+    got_inv, got_state = run(True)
+    for got_pass, want_pass in zip(got_inv, want_inv):
+        for got, want in zip(got_pass, want_pass):
+            np.testing.assert_array_equal(got, want)
+    for got, want in zip(got_state, want_state):
+        np.testing.assert_array_equal(got, want)
 
 
 def test_back_to_back_throughput_bound_inversions(hip_device):

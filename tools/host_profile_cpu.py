@@ -33,7 +33,6 @@ def main():
     layers = [m for m in net.modules() if isinstance(m, (torch.nn.Linear, torch.nn.Conv2d))]
     recs = bench.synthetic_records(bench.CONFIGS[config], batch, dev, seed=0)
     kfac = curvatures.KFAC(net)
-    kfac._stream_idle = lambda device: True
 
     def run(n):
         for _ in range(n):
