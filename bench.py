@@ -20,7 +20,15 @@ slowest rank's wall time.
 Workloads (BASELINE.json configs): N = 1 runs C2 (MLP, batch 4096, 60,000 images);
 N > 1 runs C4's per-rank shard (MLP, 8,192 rows per rank of each global batch
 N x 8,192 -- 65,536 at N = 8 -- over 65,536 images per rank); `--config lenet` is
-C3 (batch 1024), `--config wide` is C5.
+C3 (batch 1024), `--config wide` is C5.  `--strong`: SURVEY §8(e)'s strong-scaling
+pass, a fixed 65,536 x 64 images in global batches of 65,536 split over the N ranks
+(65,536 / N rows per rank and batch), "scaling": "strong".
+
+`value` is the PIPELINED rate (`metric_variant`): invert() runs on a side stream and
+its pivot verdict is read at the next invert() (KFAC.eager_verdict = False), so
+inversion k overlaps pass k+1.  `serial_images_per_s` is the reference scripts' order
+(classification_ll_block.py:93-106: a pass, then invert, its result read before the
+next pass) = images / (T_pass + T_invert).
 
 Also reported (same JSON line): the roofline of the dominant kernel
 (kfac_factor_tiles, fp32 MFMA; HIP-event durations measured live on its stream),
@@ -83,6 +91,19 @@ SHAPES = {("mlp", 1): (4096, 60000), ("mlp", 2): (8192, 65536),
           ("wide", 1): (4096, 16384), ("wide", 2): (4096, 16384)}
 BASELINE_CONFIG = {("mlp", 1): "C2", ("mlp", 2): "C4", ("lenet", 1): "C3", ("lenet", 2): "C3",
                    ("wide", 1): "C5", ("wide", 2): "C5"}
+
+
+STRONG_IMAGES, STRONG_BATCH = 65536 * 64, 65536  # SURVEY §8(e) strong-scaling pass
+
+
+def workload(config, world, strong=False):
+    """(batch per rank, images per rank) of a run: weak scaling by default (SHAPES),
+    or the fixed strong-scaling pass split over `world` ranks."""
+    if strong:
+        if config != "mlp":
+            raise ValueError("--strong is the MLP pass of SURVEY §8(e)")
+        return STRONG_BATCH // world, STRONG_IMAGES // world
+    return SHAPES[(config, 1 if world == 1 else 2)]
 
 
 def flops_per_image(layers):
@@ -167,6 +188,31 @@ def cpu_baseline(layers, images, batch, budget_s=12.0, threads=None):
                                 f"fp32, {threads} thread(s)")
 
 
+def cpu_e2e_baseline(config, images, batch, budget_s=6.0, threads=None):
+    """The reference's end-to-end CPU loop (oracle/cpu_ref_torch.e2e_pass: forward with
+    its hooks, Categorical labels, CE backward, update, invert) on a bounded sample of
+    the workload's batches; returns (images/s, threads, sample)."""
+    from oracle import cpu_ref_torch as C
+    if threads is None:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    net = build_model(config, torch.device("cpu"))
+    hooked = C.HookedCPU(net)
+    rng = np.random.default_rng(0)
+    x = torch.from_numpy(rng.random((images, *CONFIGS[config][0].in_shape), dtype=np.float32))
+    done, t0 = 0, time.perf_counter()
+    C.e2e_pass(hooked, net, x, batch, *DAMPING, max_batches=1)  # warm-up
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        d, _ = C.e2e_pass(hooked, net, x, batch, *DAMPING,
+                          max_batches=max(1, int(budget_s * 2)))
+        done += d
+    dt = time.perf_counter() - t0
+    return done / dt, threads, (f"{done} synthetic images, batch {batch}: forward + Categorical labels + "
+                                f"CE backward + update (reference hooks) + invert per group of batches, "
+                                f"torch {torch.__version__} CPU fp32, {threads} thread(s)")
+
+
 def load_traffic(config):
     name = "factor_tiles_pmc.json" if config == "mlp" else f"factor_tiles_pmc_{config}.json"
     path = os.path.join(ROOT, "profiles", name)
@@ -239,6 +285,8 @@ def main(argv=None):
     ap.add_argument("--config", default="mlp", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="per-rank batch (default: the config's)")
     ap.add_argument("--images", type=int, default=None, help="images per rank per pass")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: 65,536 x 64 images in global batches of 65,536 over the N ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-serial", action="store_true")
@@ -267,7 +315,7 @@ def main(argv=None):
               f"visible", file=sys.stderr, flush=True)
         return 2
     shape_key = (args.config, 1 if world == 1 else 2)
-    batch, images = SHAPES[shape_key]
+    batch, images = workload(args.config, world, args.strong)
     batch = args.batch or batch
     images = args.images or images
 
@@ -446,17 +494,29 @@ def main(argv=None):
         cpu = {"value": v, "unit": "images/s", "cores": cores, "kind": "port", "sample": sample,
                "value_1_thread": v1, "sample_1_thread": sample1, "cpu_model": cpu_model(),
                "logical_cpus_visible": os.cpu_count()}
+        if args.config == "mlp":
+            # BASELINE C1: the reference's CPU pass at ITS batch (256), and the CPU
+            # end-to-end loop beside the GPU's e2e_images_per_s
+            vc1, _, samplec1 = cpu_baseline(specs, 60000, 256, budget_s=6.0)
+            ve, _, samplee = cpu_e2e_baseline(args.config, 60000, 256)
+            cpu.update({"c1_batch256_value": vc1, "c1_batch256_sample": samplec1,
+                        "e2e_value": ve, "e2e_sample": samplee})
 
     if rank == 0:
         cfg = BASELINE_CONFIG[shape_key]
         out = {"metric": METRIC, "value": value, "unit": "images/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
-               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+               "higher_is_better": True, "scaling": "strong" if args.strong else "weak",
+               "vs_baseline": None, "dtype": "f32",
+               "metric_variant": ("pipelined: inversion k overlaps pass k+1 (eager_verdict=False); "
+                                  "serial_images_per_s = images / (T_pass + T_invert), the "
+                                  "reference scripts' order"),
                "data": "synthetic (resident U[0,1) activations, N(0,1) output-gradient records)",
                "config": {"workload": f"{cfg}: {NAMES[args.config]} KFAC factor pass over {images} "
                                       f"images/rank (batch {batch}/rank, global batch {batch * world}) "
                                       f"+ invert{DAMPING}",
-                          "baseline_config": cfg, "global_batch": batch * world,
+                          "baseline_config": cfg + (" strong" if args.strong else ""),
+                          "global_batch": batch * world,
                           "images_per_rank": images, "parallelism": f"dp{world}",
                           "inversion": ("sharded" if getattr(kfac, "_sharded_last", False)
                                         else "replicated")},

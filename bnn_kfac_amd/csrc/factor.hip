@@ -431,6 +431,326 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
 #define kfac_factor_tiles_channel kfac_factor_tiles_t<32, 2, false, KFAC_CHANNEL>
 #define kfac_factor_tiles_patch kfac_factor_tiles_t<32, 2, false, KFAC_PATCH>
 
+// ------------------------------------------------- bf16x3 split SYRK (row-major)
+// fp32-accurate products on the bf16 matrix cores.  Every operand element is split
+// EXACTLY into three bf16 parts, x = x1 + x2 + x3 (round-to-nearest splits: x1 holds
+// the top 8 significant bits, x2 the next 8, x3 the last 8 of fp32's 24), and
+//   x_a x_b = x1a x1b + (x1a x2b + x2a x1b) + (x1a x3b + x2a x2b + x3a x1b) + O(2^-24)
+// -- six bf16 MFMA products per fp32 product, the dropped terms (x2 x3, x3 x2, x3 x3)
+// below fp32's own rounding of the product, accumulated in fp32 by the MFMA.  On
+// gfx950 v_mfma_f32_32x32x16_bf16 retires 16x the FLOP/cycle of the fp32 MFMA
+// (v_mfma_f32_32x32x2_f32), so six of them are 2.67x the fp32 MFMA rate: the
+// roofline of this kernel is 2.5 PF / 6 = 417 TF/s of fp32-equivalent work.
+//
+// Work unit: one 128 x 128 macro tile (= 2 x 2 of the 64-tiles whose partial slabs
+// the reduce sums) of one factor over one K-chunk; one workgroup per CU (96 KB of
+// LDS), 512 threads in two roles, one of each per SIMD:
+//   consumers (waves 0-3): wave w computes the 64 x 64 quadrant (w >> 1, w & 1) =
+//     2 x 2 blocks of 32 x 32 -- fragment reads and MFMAs only;
+//   producers (waves 4-7): load the next stage's rows, split them into the three
+//     bf16 parts and store them -- global loads, VALU and LDS stores only,
+// so each SIMD's MFMA pipe is fed by one wave while the other does the conversion
+// work beside it; one barrier per stage hands the stage over (double-buffered).
+// A stage = 32 rows of K; a producer thread takes 8 rows of 2 columns of the A
+// panel and the same of the B panel.  LDS image per stage: two substep regions
+// (k 0-15, 16-31), each [part][column][2 chunks of 8 k] (32 B per column, k
+// contiguous), read straight into MFMA operands (lane = column, 8 k per
+// ds_read_b128).  The chunk of a column is XOR-swizzled by bit 3 of the column and
+// the second region is offset by 64 B mod 128: fragment reads and the stores are
+// both conflict-free, and every fragment read is a per-lane base plus an immediate.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int MT = 128;                          // macro tile edge
+constexpr int S3_THREADS = 512;
+constexpr int S3_PART = 2 * MT * 32;             // bytes of one part of one substep region
+constexpr int S3_REG = 3 * S3_PART + 64;         // substep region (+64: store banks)
+constexpr int S3_STAGE = 2 * S3_REG;
+constexpr int S3_LDS = 2 * S3_STAGE;             // two stages: 98,560 bytes
+
+// byte offset of half-chunk hh (k 8hh .. 8hh+7 of a substep) of column c in a part
+__device__ __forceinline__ int s3_half(int c, int hh) { return c * 32 + ((hh ^ ((c >> 3) & 1)) << 4); }
+
+// (a, b) -> bf16 pair (a low), round to nearest even.  Inline asm: from a plain
+// cast the compiler re-derives (pair << 16) as a second conversion of (a, 0)
+__device__ __forceinline__ uint32_t bf16_pair(float a, float b) {
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// x - y as one v_sub_f32 (the compiler would pair the subtractions into
+// v_pk_add_f32, which costs ~6x its issue slot beside MFMAs on gfx950)
+__device__ __forceinline__ float sub_f32(float x, float y) {
+  float r;
+  asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+  return r;
+}
+
+// (a, b) -> their hi / mid / lo bf16 parts, packed as pairs (a low, b high)
+__device__ __forceinline__ void split3(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = bf16_pair(a, b);
+  const float ra = sub_f32(a, __uint_as_float(h << 16)), rb = sub_f32(b, __uint_as_float(h & 0xffff0000u));
+  m = bf16_pair(ra, rb);
+  const float sa = sub_f32(ra, __uint_as_float(m << 16)), sb = sub_f32(rb, __uint_as_float(m & 0xffff0000u));
+  l = bf16_pair(sa, sb);
+}
+
+// A producer thread's share of a stage: rows 8q .. 8q+7 of columns (panel 0: A,
+// 1: B) 4g + e and 4g + e + 2.  S3_DEPTH stages of loads are in flight (register
+// ring): the rows come from L2 / the Infinity Cache, ~1 us away, and a stage
+// computes in about that.
+constexpr int S3_DEPTH = 3;
+struct S3Prod {
+  int vob[2][8];      // byte offset of row 8q + r of the panel's first column (OOB: fill)
+  float fill[2];      // 1 for the bias ones column, else 0 (first column of a panel)
+  int off0, off1;     // LDS byte offsets of the two columns' chunks (A panel; B: + 128 columns)
+  int q;
+};
+typedef float S3Rows[2][2][8];  // [panel][column][row] of one stage
+
+// loads of the stage at `cur` into v: raw buffer loads of the stage's rows (base and
+// size uniform, from SGPRs) at per-thread byte offsets; rows past the batch and fill
+// columns fall outside the buffer and read 0; the ones column adds its 1.
+template <int NP>
+__device__ __forceinline__ void s3_load(const S3Prod& P, S3Rows& v, const FactorJobDev& J,
+                                        const float* const* segs, StageCursor& cur, int ld) {
+  const uint64_t bpu = reinterpret_cast<uint64_t>(seg_base(J, segs, cur.seg) + cur.k * ld);
+  // (uniform by construction; readfirstlane tells the compiler, else it wraps every
+  // buffer load in a waterfall loop.  readfirstlane returns int: zero-extend)
+  void* bp = reinterpret_cast<void*>(
+      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(bpu >> 32)) << 32) |
+      (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)bpu));
+  const int64_t left = J.x.rows - cur.k;
+  const int nrow = __builtin_amdgcn_readfirstlane(left < BK ? (int)left : BK);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      bp, (short)0, __builtin_amdgcn_readfirstlane(nrow * ld * 4), 0x00020000);
+#pragma unroll
+  for (int pn = 0; pn < NP; ++pn)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      v[pn][0][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, P.vob[pn][r], 0, 0));
+      v[pn][1][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, P.vob[pn][r] + 8, 0, 0));
+    }
+  // the ones column: 1 on the stage's real rows (added once the loads have landed:
+  // the values are kept as an offset until the commit)
+  (void)nrow;
+  cur.next(J.x.rows);
+}
+
+// v -> hi / mid / lo parts -> the thread's chunks of a stage (`nrow` real rows)
+template <int NP>
+__device__ __forceinline__ void s3_commit(const S3Prod& P, S3Rows& v, int nrow, char* stage) {
+#pragma unroll
+  for (int pn = 0; pn < NP; ++pn)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[pn][0][r] += (8 * P.q + r < nrow) ? P.fill[pn] : 0.f;
+#pragma unroll
+  for (int pn = 0; pn < NP; ++pn)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      uint32_t h[4], m[4], l[4];
+#pragma unroll
+      for (int r2 = 0; r2 < 4; ++r2) split3(v[pn][c][2 * r2], v[pn][c][2 * r2 + 1], h[r2], m[r2], l[r2]);
+      char* d = stage + (c ? P.off1 : P.off0) + pn * MT * 32;
+      *reinterpret_cast<uint4*>(d) = make_uint4(h[0], h[1], h[2], h[3]);
+      *reinterpret_cast<uint4*>(d + S3_PART) = make_uint4(m[0], m[1], m[2], m[3]);
+      *reinterpret_cast<uint4*>(d + 2 * S3_PART) = make_uint4(l[0], l[1], l[2], l[3]);
+    }
+}
+
+// A consumer wave's MFMAs on one stage: blocks (bi, bj) of its 64 x 64 quadrant with
+// act[bi][bj], six products per block and k-16 substep.  oa / ob: this lane's A / B
+// fragment offsets (substep 0, part 0, block 0); everything else is an immediate.
+__device__ __forceinline__ void s3_consume(const char* stage, int oa, int ob, const bool (&act)[2][2],
+                                           floatx16 (&acc)[2][2]) {
+  auto frag = [&](int off) { return *reinterpret_cast<const bf16x8*>(stage + off); };
+  bf16x8 a[2][2][3], b[2][2][3];  // [substep][block][part]
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        a[s][x][p] = frag(oa + s * S3_REG + p * S3_PART + x * 32 * 32);
+        b[s][x][p] = frag(ob + s * S3_REG + p * S3_PART + x * 32 * 32);
+      }
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj) {
+        if (!act[bi][bj]) continue;
+        const bf16x8 *A = a[s][bi], *B = b[s][bj];
+        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], acc[bi][bj], 0, 0, 0);
+        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[1], acc[bi][bj], 0, 0, 0);
+        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[2], acc[bi][bj], 0, 0, 0);
+        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0], acc[bi][bj], 0, 0, 0);
+        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], acc[bi][bj], 0, 0, 0);
+        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], acc[bi][bj], 0, 0, 0);
+      }
+}
+
+// Macro tile of a unit index, in blocks of 4 tile rows x 8 tile columns of the lower
+// triangle: the ~32 tasks an XCD runs at once (xcd_task hands it a contiguous range)
+// then read 4 A panels and 8 B panels, not 1 and 32, so a stage's rows are fetched
+// into its L2 once per panel block instead of once per task (wide factors: 4096
+// columns = 32 panels of 128 each far larger than the 4 MB L2).
+__device__ __forceinline__ void s3_decode(int unit, int T3, int& I, int& J) {
+  int base = 0;
+  I = J = 0;
+  for (int i0 = 0; i0 < T3; i0 += 4) {
+    const int i1 = min(T3, i0 + 4);
+    for (int j0 = 0; j0 < i1; j0 += 8) {
+      int cnt = 0;
+      for (int i = i0; i < i1; ++i) cnt += max(0, min(j0 + 8, i + 1) - j0);
+      if (unit < base + cnt) {
+        int r = unit - base;
+        for (int i = i0; i < i1; ++i) {
+          const int w = max(0, min(j0 + 8, i + 1) - j0);
+          if (r < w) {
+            I = i;
+            J = j0 + r;
+            return;
+          }
+          r -= w;
+        }
+      }
+      base += cnt;
+    }
+  }
+}
+
+__device__ __forceinline__ void s3_task(const FactorJobDev& J, const float* const* segs, int local,
+                                        char* lds) {
+  const int T3 = (J.n + MT - 1) / MT, units = T3 * (T3 + 1) / 2;
+  const int split = local / units, unit = local - split * units;
+  int I, Jc;
+  s3_decode(unit, T3, I, Jc);
+  const bool same = I == Jc;
+  const int64_t s0 = (int64_t)split * J.chunk;
+  const int64_t s1 = min(J.nst, s0 + J.chunk);
+  const int ns = (int)(s1 - s0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (wave < 4) {
+    // ---------------------------------------------------------------- consumer
+    const int wr = wave >> 1, wc = wave & 1;
+    bool act[2][2];
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj) {
+        const int r0 = I * MT + wr * 64 + bi * 32, c0 = Jc * MT + wc * 64 + bj * 32;
+        act[bi][bj] = r0 < J.n && c0 < J.n && r0 >= c0;
+      }
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[bi][bj][v] = 0.f;
+    const int cl = lane & 31, lo = s3_half(cl, lane >> 5);
+    const int oa = wr * 64 * 32 + lo;
+    const int ob = ((same ? 0 : MT) + wc * 64) * 32 + lo;
+    const bool any = act[0][0] || act[0][1] || act[1][0] || act[1][1];
+    if (ns > 0) {
+      __syncthreads();  // stage 0 stored
+      for (int st = 0; st < ns; ++st) {
+        if (any) s3_consume(lds + (st & 1) * S3_STAGE, oa, ob, act, acc);
+        __syncthreads();  // stage st read; stage st+1 stored
+      }
+    }
+    // partials -> the 64-tile slabs: block (bi, bj) = quadrant (bi, bj) of 64-tile
+    // (2I + wr, 2Jc + wc)
+    const int ti = 2 * I + wr, tj = 2 * Jc + wc;
+    float* o = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.splits + split) * TILE * TILE;
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj)
+        if (act[bi][bj])
+          put_partial(J, acc[bi][bj],
+                      [&](int v) { return &o[(bi * 32 + acc_row(v, lane)) * TILE + bj * 32 + (lane & 31)]; });
+    return;
+  }
+  // ---------------------------------------------------------------- producer
+  if (ns <= 0) return;
+  // thread p -> row chunk q = p & 3 and columns 4g + e, 4g + e + 2 (g = p >> 3, e = (p >> 2) & 1)
+  // of each panel: the 8 lanes of a ds_write_b128 group cover both column parities x
+  // 4 chunks (conflict-free stores).  A diagonal tile loads its one panel.
+  const int p = tid - 256, q = p & 3, g = p >> 3, e = (p >> 2) & 1;
+  const int ld = __builtin_amdgcn_readfirstlane((int)J.x.ld);  // (< 2^24: a stage's offsets fit 32 bits)
+  S3Prod P;
+  P.q = q;
+  P.off0 = (q >> 1) * S3_REG + s3_half(4 * g + e, q & 1);
+  P.off1 = (q >> 1) * S3_REG + s3_half(4 * g + e + 2, q & 1);
+#pragma unroll
+  for (int pn = 0; pn < 2; ++pn) {
+    const int col = (pn ? Jc : I) * MT + 4 * g + e;
+    const bool real = col < J.x.cols;  // cols % 4 == 0: a 4-column group is all real or all fill
+    P.fill[pn] = (col == J.x.ones) ? 1.f : 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) P.vob[pn][r] = real ? ((8 * q + r) * ld + col) * 4 : 0x7fffff00;
+  }
+  StageCursor cur;
+  cur.init(J, s0);
+  // real rows of stage i (its loads are in flight until its commit): the ring's
+  // stages are consecutive, so they are tracked with a second cursor
+  StageCursor rc = cur;
+  auto rows_of = [&]() {
+    const int64_t left = J.x.rows - rc.k;
+    const int nrow = __builtin_amdgcn_readfirstlane(left < BK ? (int)left : BK);
+    rc.next(J.x.rows);
+    return nrow;
+  };
+  auto run = [&](auto npc) {
+    constexpr int NP = decltype(npc)::value;
+    S3Rows v[S3_DEPTH];
+    // stage i lives in ring slot i % S3_DEPTH; the loop is unrolled by the ring depth
+    // so every slot is a fixed register set
+#pragma unroll
+    for (int i = 0; i < S3_DEPTH; ++i)
+      if (i < ns) s3_load<NP>(P, v[i], J, segs, cur, ld);
+    s3_commit<NP>(P, v[0], rows_of(), lds);
+    if (S3_DEPTH < ns) s3_load<NP>(P, v[0], J, segs, cur, ld);
+    __syncthreads();  // stage 0 stored
+    for (int st0 = 0; st0 < ns; st0 += S3_DEPTH) {
+#pragma unroll
+      for (int u = 0; u < S3_DEPTH; ++u) {
+        const int st = st0 + u;  // consumers compute stage st; store stage st+1
+        if (st >= ns) break;
+        if (st + 1 < ns) {
+          constexpr int dummy = 0;
+          (void)dummy;
+          S3Rows& nx = v[(u + 1) % S3_DEPTH];
+          s3_commit<NP>(P, nx, rows_of(), lds + ((st + 1) & 1) * S3_STAGE);
+          if (st + 1 + S3_DEPTH < ns) s3_load<NP>(P, nx, J, segs, cur, ld);
+        }
+        __syncthreads();
+      }
+    }
+  };
+  if (same) run(std::integral_constant<int, 1>{});
+  else run(std::integral_constant<int, 2>{});
+}
+
+__global__ __launch_bounds__(S3_THREADS, 1) void kfac_factor_syrk3(FactorArgs args) {
+  extern __shared__ __attribute__((aligned(16))) char s3lds[];
+  const int task = xcd_task(blockIdx.x, gridDim.x);
+  int j = 0;
+  while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
+  const FactorJobDev& J = args.job[j];
+  const int local = task - J.task_begin;
+  if (J.n <= 32) {
+    if (threadIdx.x < NTHREADS)  // the 4-wave narrow path (its barriers count 4 waves:
+      // the other 4 leave first, so they never meet a barrier)
+      factor_task_narrow_direct(J, args.segs, local, reinterpret_cast<float*>(s3lds));
+  } else {
+    s3_task(J, args.segs, local, s3lds);
+  }
+}
+
 // ------------------------------------------------------------ conv operands
 // Conv2d factors with each image staged whole in LDS (replaces the per-element
 // register gather of the im2col / channel-major panel loaders for images that fit).
@@ -1002,18 +1322,44 @@ static bool job_glds(const kfac_factor_job& jb) {
          (jb.x.ld % 4) == 0 && (reinterpret_cast<uintptr_t>(jb.x.ptr) % 16) == 0;
 }
 
+// bf16x3 SYRK (kfac_factor_syrk3) for a row-major launch group: every job either
+// LDS-eligible (16-byte rows, n > 32) or narrow (n <= 32, direct loads).
+// KFAC_SYRK3=1 selects it (default: the fp32-MFMA kernel until it wins the A/B).
+static bool syrk3_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("KFAC_SYRK3");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+
+static bool syrk3_group(const kfac_factor_job* jobs, int njobs) {
+  if (!syrk3_enabled() || njobs <= 0) return false;
+  bool big = false;
+  for (int i = 0; i < njobs; ++i) {
+    if (jobs[i].x.layout != KFAC_ROWMAJOR) return false;
+    const int n = factor_n(jobs[i]);
+    if (n > 32 && !job_glds(jobs[i])) return false;
+    big |= n > 32;
+  }
+  return big;
+}
+
 static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
                       int64_t slots = 0) {
-  // resident workgroups per CU: 4 (32 KB of LDS each)
-  if (slots <= 0) slots = 4 * 256;
+  const bool s3 = syrk3_group(jobs, njobs);
+  // resident workgroups per CU: 4 (32 KB of LDS each); the bf16x3 kernel: 1 (96 KB)
+  if (slots <= 0) slots = (s3 ? 1 : 4) * 256;
   constexpr int64_t MIN_CHUNK = 8, OVERHEAD = 4;  // stages; ~per-task fixed cost in stages
   int64_t max_steps = 1;
   for (int i = 0; i < njobs; ++i) max_steps = std::max(max_steps, job_stages(jobs[i]));
   int64_t units[MAXJ];
   for (int i = 0; i < njobs; ++i) {
     const int64_t t = cdiv(factor_n(jobs[i]), TILE);
+    const int64_t t3 = cdiv(factor_n(jobs[i]), MT);
     ConvGeom cg;
-    units[i] = conv_geom(jobs[i], cg) ? cg.units : t * (t + 1) / 2;
+    if (s3) units[i] = factor_n(jobs[i]) <= 32 ? 1 : t3 * (t3 + 1) / 2;
+    else units[i] = conv_geom(jobs[i], cg) ? cg.units : t * (t + 1) / 2;
   }
   // workgroups of job i at `splits` K-splits
   auto job_tasks = [&](int i, int64_t splits) { return units[i] * splits; };
@@ -1210,7 +1556,13 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
         {
           bool all_glds = true;
           for (int i = 0; i < njobs; ++i) all_glds &= args.job[i].glds != 0 || args.job[i].n <= 32;
-          if (all_glds)
+          if (syrk3_group(jobs, njobs)) {
+            static const bool attr = hipFuncSetAttribute(
+                reinterpret_cast<const void*>(&kfac_factor_syrk3),
+                hipFuncAttributeMaxDynamicSharedMemorySize, S3_LDS) == hipSuccess;
+            if (!attr) return KFAC_ELAUNCH;
+            hipLaunchKernelGGL(kfac_factor_syrk3, dim3(tasks), dim3(S3_THREADS), S3_LDS, stream, args);
+          } else if (all_glds)
             hipLaunchKernelGGL(kfac_factor_tiles_glds, dim3(tasks), dim3(NTHREADS), 0, stream, args);
           else
             hipLaunchKernelGGL(kfac_factor_tiles, dim3(tasks), dim3(NTHREADS), 0, stream, args);

@@ -13,6 +13,10 @@ reference itself does not travel:
 * invert  (curvatures.py:374-398): R = s**0.5 * F + diag(n**0.5); R = (R + R^T)/2;
   L = R.inverse().cholesky()  (torch.linalg.inv + torch.linalg.cholesky, the
   non-deprecated names of the same LAPACK getrf/getri + potrf calls).
+* end to end (classification_ll_block.py:93-106): forward with the reference's
+  hooks recording the layer inputs (curvatures.py:319-320) and grad_output * B
+  (:322-323), a Categorical label draw, cross-entropy backward, the update above
+  per batch, then invert.
 """
 from __future__ import annotations
 
@@ -60,3 +64,49 @@ def invert(state: dict, add=0.0, multiply=1.0) -> dict:
             out.append(torch.linalg.cholesky(torch.linalg.inv(R)))
         inv[name] = tuple(out)
     return inv
+
+
+class HookedCPU:
+    """The reference's hooks on a CPU model (curvatures.py:310-323): forward pre-hook
+    keeps the input, backward hook keeps grad_output[0] * batch."""
+
+    def __init__(self, model):
+        self.layers = [m for m in model.modules() if isinstance(m, (torch.nn.Linear, torch.nn.Conv2d))]
+        self.record = {m: [None, None] for m in self.layers}
+        for m in self.layers:
+            m.register_forward_pre_hook(self._save_input)
+            m.register_full_backward_hook(self._save_output)
+
+    def _save_input(self, module, inp):
+        self.record[module][0] = inp[0]
+
+    def _save_output(self, module, grad_input, grad_output):
+        self.record[module][1] = grad_output[0] * grad_output[0].size(0)
+
+    def update(self, state):
+        for i, m in enumerate(self.layers):
+            a, g = self.record[m]
+            if isinstance(m, torch.nn.Conv2d):
+                conv_update(state, i, a.detach(), g.detach(), m.kernel_size, m.padding, m.stride,
+                            m.bias is not None)
+            else:
+                linear_update(state, i, a.detach(), g.detach(), m.bias is not None)
+
+
+def e2e_pass(hooked: HookedCPU, model, x: torch.Tensor, batch: int, add: float, multiply: float,
+             max_batches: int = None):
+    """One pass of classification_ll_block.py:93-106 on the CPU; returns (images, inv)."""
+    state, done = {}, 0
+    crit = torch.nn.CrossEntropyLoss()
+    for bi, i in enumerate(range(0, x.shape[0], batch)):
+        if max_batches is not None and bi >= max_batches:
+            break
+        xb = x[i:i + batch]
+        logits = model(xb)
+        labels = torch.distributions.Categorical(logits=logits).sample()
+        loss = crit(logits, labels)
+        model.zero_grad()
+        loss.backward()
+        hooked.update(state)
+        done += xb.shape[0]
+    return done, invert(state, add, multiply)

@@ -84,3 +84,17 @@ def test_workload_shapes():
     assert bench.SHAPES[("lenet", 1)][0] == 1024
     assert bench.flops_per_image(bench.CONFIGS["mlp"]) == 650402
     assert bench.flops_per_image(bench.CONFIGS["lenet"]) == 3110740
+
+
+def test_strong_scaling_workload():
+    # 65,536 x 64 images in global batches of 65,536, split over N ranks
+    for n in (1, 2, 4, 8):
+        batch, images = bench.workload("mlp", n, strong=True)
+        assert batch * n == 65536 and images * n == 65536 * 64
+    assert bench.workload("mlp", 1) == bench.SHAPES[("mlp", 1)]
+    assert bench.workload("mlp", 4) == bench.SHAPES[("mlp", 2)]
+
+
+def test_cpu_e2e_baseline_runs():
+    v, threads, sample = bench.cpu_e2e_baseline("mlp", 1024, 256, budget_s=0.2, threads=1)
+    assert v > 0 and threads == 1 and "Categorical" in sample
