@@ -31,7 +31,8 @@ inversion k overlaps pass k+1.  `serial_images_per_s` is the reference scripts' 
 next pass) = images / (T_pass + T_invert).
 
 Also reported (same JSON line): the roofline of the dominant kernel
-(kfac_factor_tiles, fp32 MFMA; HIP-event durations measured live on its stream),
+(kfac_factor_tiles, fp32 MFMA, or kfac_factor_syrk3, bf16x3 MFMA, for the wide
+config's n >= 2048 factors; HIP-event durations measured live on its stream),
 the pass/all-reduce/invert split, the serial rate (one pass, then invert on the
 caller's stream, then the verdict read: the latency a caller who does not pipeline
 passes sees), an end-to-end variant (forward + Categorical label sample + CE
@@ -56,6 +57,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "images/sec for full KFAC factor pass + factor inversion, MNIST MLP, 1/2/4/8 GPUs"
 MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md, chip table)
+# kfac_factor_syrk3 computes each fp32 product as six bf16 MFMA products (exact bf16x3
+# split): its roofline is the dense bf16 MFMA peak / 6 in fp32-equivalent flops
+MFMA_BF16_PEAK_TFLOPS = 2500.0
+SYRK3_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / 6
 DAMPING = (0.2 ** 2, 200)     # invert(std**2, N), classification_ll_block.py:72-73,106
 
 
@@ -410,6 +415,13 @@ def main(argv=None):
     comm["timing"] = False
     N.profile_enable(False)
     tiles_ms, tiles_n = N.profile_read(N.PROF_FACTOR_TILES)
+    s3_ms, s3_n = N.profile_read(N.PROF_FACTOR_SYRK3)
+    # the dominant factor kernel: the bf16x3 SYRK takes launch groups with a factor of
+    # n >= 2048 (wide), the fp32-MFMA kernel the rest
+    syrk3 = s3_ms > tiles_ms
+    f32_ms = tiles_ms
+    if syrk3:
+        tiles_ms, tiles_n = s3_ms, s3_n
     red_ms, red_n = N.profile_read(N.PROF_FACTOR_REDUCE)
     inv_ms, inv_n = N.profile_read(N.PROF_INVERT)
     N.profile_reset()
@@ -427,17 +439,21 @@ def main(argv=None):
     fpi = flops_per_image(specs)
     flops_timed = fpi * images * args.steps
     achieved = flops_timed / (tiles_ms * 1e-3) / 1e12 if tiles_ms > 0 else None
-    roofline = {"bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": (achieved / MFMA_F32_PEAK_TFLOPS) if achieved else None,
+    peak = SYRK3_PEAK_TFLOPS if syrk3 else MFMA_F32_PEAK_TFLOPS
+    roofline = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                "frac": (achieved / peak) if achieved else None,
                 "traffic": load_traffic(args.config),
-                "kernel": "kfac_factor_tiles", "launches": tiles_n,
+                "kernel": "kfac_factor_syrk3" if syrk3 else "kfac_factor_tiles",
+                "peak_basis": ("dense bf16 MFMA 2.5 PF / 6 products per fp32 product (fp32-equivalent)"
+                               if syrk3 else "dense fp32 MFMA"),
+                "launches": tiles_n,
                 "avg_launch_us": 1e3 * tiles_ms / max(tiles_n, 1),
                 # a launch covers every queued update of the pass (multi-batch jobs):
                 # per-launch figures are the step's algorithmic totals / its launches
                 "flops_per_launch": fpi * images * args.steps / max(tiles_n, 1),
                 "algorithmic_bytes_per_launch": bytes_per_image(specs) * images * args.steps
                                                 / max(tiles_n, 1)}
-    breakdown = {"factor_tiles_ms_per_step": tiles_ms / args.steps,
+    breakdown = {"factor_tiles_ms_per_step": (tiles_ms + (f32_ms if syrk3 else s3_ms)) / args.steps,
                  "factor_reduce_ms_per_step": red_ms / args.steps,
                  "invert_ms_per_step": inv_ms / args.steps,
                  "allreduce_ms_per_step": allreduce_ms,

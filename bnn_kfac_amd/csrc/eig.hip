@@ -245,6 +245,8 @@ struct TriArgs {
   int64_t ldF;
   int n, G, R;         // rows per workgroup R = ceil(n / G)
   double* rows_g;      // G x R x n owned rows when they do not fit LDS (else null)
+  double* vecs_g;      // G x 3n: each workgroup's x / u / w vectors when 3n doubles do not
+                       // fit LDS (n > 6400; else null)
   gran_t* pub;         // 2 (step parity) x n x 4 granules {p lo, p hi, a lo, a hi}
   unsigned* abort;     // timeout flag
   double* d;           // n: diagonal of T
@@ -333,10 +335,13 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 
 constexpr int TRI_CH = 8;  // columns per thread per sweep (4 granules each)
 
-template <bool LDS_ROWS, int RB>
+template <bool LDS_ROWS, int RB, bool VEC_LDS = true>
 __global__ __launch_bounds__(NTHREADS) void eig_tridiag(TriArgs a) {
   constexpr int TB = NTHREADS, W = TB / 64, CH = TRI_CH;
-  extern __shared__ double lds[];  // [v0 n][v1 n][w n][rows R x n if LDS_ROWS]
+  // [v0 n][v1 n][w n][rows R x n if LDS_ROWS]; without VEC_LDS (n > 6400: 3n doubles
+  // exceed the LDS budget) the vectors are this workgroup's private global slab
+  extern __shared__ double lds_dyn[];
+  double* lds = VEC_LDS ? lds_dyn : a.vecs_g + (size_t)blockIdx.x * 3 * a.n;
   __shared__ double red[TB / 64];
   __shared__ int fail_s;
   const int n = a.n, G = a.G, wg = blockIdx.x, tid = threadIdx.x;
@@ -345,7 +350,7 @@ __global__ __launch_bounds__(NTHREADS) void eig_tridiag(TriArgs a) {
   // slot; w is rewritten after each row pass (the previous w is dead by then)
   double* vs[2] = {lds, lds + n};
   double* wS = lds + 2 * n;
-  double* rows = LDS_ROWS ? lds + 3 * n : a.rows_g + (size_t)wg * a.R * n;
+  double* rows = LDS_ROWS ? lds_dyn + (VEC_LDS ? 3 * n : 0) : a.rows_g + (size_t)wg * a.R * n;
   auto row_of = [&](int slot) { return slot * G + wg; };
   auto A = [&](int slot) { return rows + (size_t)slot * n; };
   if (tid == 0) fail_s = 0;
@@ -611,9 +616,13 @@ __global__ __launch_bounds__(NTHREADS) void eig_tridiag(TriArgs a) {
 // recurrence reach fp64 resolution, where one-point bisection needs ~55 (the
 // recurrence is a chain of dependent fp64 divisions, so rounds, not flops, are the
 // cost).  d and e^2 are staged in LDS once per workgroup.
+template <bool SH>
 __global__ __launch_bounds__(NTHREADS) void eig_bisect(const double* d, const double* e, int n,
                                                        double* evals, const unsigned* abort, int* info) {
-  extern __shared__ double sh[];  // [d n][e^2 n]
+  // [d n][e^2 n] in LDS; without SH (n > 9600) d and e are read from global memory
+  // (every lane of a wave reads the same element: one broadcast access) and e^2 is
+  // formed in the loop
+  extern __shared__ double sh[];
   double* dS = sh;
   double* e2S = sh + n;
   __shared__ double red[2][NTHREADS / 64];
@@ -622,8 +631,10 @@ __global__ __launch_bounds__(NTHREADS) void eig_bisect(const double* d, const do
   double lo = 0.0, hi = 0.0, emax2 = 0.0;
   for (int i = tid; i < n; i += NTHREADS) {
     const double di = d[i], ei = i + 1 < n ? e[i] : 0.0;
-    dS[i] = di;
-    e2S[i] = ei * ei;
+    if (SH) {
+      dS[i] = di;
+      e2S[i] = ei * ei;
+    }
     const double r = (i > 0 ? fabs(e[i - 1]) : 0.0) + fabs(ei);
     lo = i == tid ? di - r : fmin(lo, di - r);
     hi = i == tid ? di + r : fmax(hi, di + r);
@@ -659,7 +670,7 @@ __global__ __launch_bounds__(NTHREADS) void eig_bisect(const double* d, const do
     const double mid = lane == 63 ? hi - step : lo + step * (double)(lane + 1);
     // count of eigenvalues < mid (LDL^T inertia)
     int cnt = 0;
-    double q = dS[0] - mid;
+    double q = (SH ? dS[0] : d[0]) - mid;
     if (fabs(q) < pivmin) q = -pivmin;
     cnt += q < 0.0;
     for (int i = 1; i < n; ++i) {
@@ -669,7 +680,7 @@ __global__ __launch_bounds__(NTHREADS) void eig_bisect(const double* d, const do
       double r = __builtin_amdgcn_rcp(q);
       r = fma(r, fma(-q, r, 1.0), r);
       r = fma(r, fma(-q, r, 1.0), r);
-      q = (dS[i] - mid) - e2S[i - 1] * r;
+      q = SH ? (dS[i] - mid) - e2S[i - 1] * r : (d[i] - mid) - (e[i - 1] * e[i - 1]) * r;
       if (fabs(q) < pivmin) q = -pivmin;
       cnt += q < 0.0;
     }
@@ -787,45 +798,55 @@ __global__ __launch_bounds__(NTHREADS) void eig_tri_vectors(const double* d, con
 // Back-transform: v_j = H_0 H_1 ... H_{n-3} z_j (T = Q^T A Q, Q = H_0 ... H_{n-3}).
 // Columns are independent, so each block carries 4 eigenvectors through all the
 // reflectors in LDS with no grid synchronisation; output fp32 evecs[i][j].
-constexpr int BT_VECS = 4;
-
+// V vectors per block.  VS_LDS: the V columns staged in LDS (8 V n bytes: V = 4 up to
+// n = 4800, 2 up to 9600, 1 up to 19200); beyond that the one column is updated in
+// place in Z (strided, uncached -- n > 19200 is far past any layer the reference's
+// scripts build)
+template <int V, bool VS_LDS>
 __global__ __launch_bounds__(NTHREADS) void eig_backtransform(const double* U, const double* tau,
-                                                              const double* Z, int n, float* evecs,
+                                                              double* Z, int n, float* evecs,
                                                               int64_t ldv) {
-  extern __shared__ double vs[];  // BT_VECS x n
-  __shared__ double red[BT_VECS][NTHREADS / 64];
-  const int j0 = blockIdx.x * BT_VECS, tid = threadIdx.x;
-  const int nv = min(BT_VECS, n - j0);
-  for (int q = 0; q < BT_VECS; ++q)
-    for (int i = tid; i < n; i += NTHREADS) vs[q * n + i] = q < nv ? Z[(size_t)i * n + j0 + q] : 0.0;
-  __syncthreads();
+  extern __shared__ double vs_dyn[];
+  __shared__ double red[V][NTHREADS / 64];
+  const int j0 = blockIdx.x * V, tid = threadIdx.x;
+  const int nv = min(V, n - j0);
+  auto vs = [&](int q, int i) -> double& {
+    return VS_LDS ? vs_dyn[q * n + i] : Z[(size_t)i * n + j0 + q];
+  };
+  if (VS_LDS) {
+    for (int q = 0; q < V; ++q)
+      for (int i = tid; i < n; i += NTHREADS) vs(q, i) = q < nv ? Z[(size_t)i * n + j0 + q] : 0.0;
+    __syncthreads();
+  }
   for (int k = n - 3; k >= 0; --k) {
     const double t = tau[k];
     if (t == 0.0) continue;  // uniform
     const double* u = U + (size_t)k * n;
-    double s[BT_VECS] = {0.0, 0.0, 0.0, 0.0};
+    double s[V];
+#pragma unroll
+    for (int q = 0; q < V; ++q) s[q] = 0.0;
     for (int i = k + 1 + tid; i < n; i += NTHREADS) {
       const double ui = u[i];
 #pragma unroll
-      for (int q = 0; q < BT_VECS; ++q) s[q] += ui * vs[q * n + i];
+      for (int q = 0; q < V; ++q) s[q] += ui * vs(q, i);
     }
 #pragma unroll
-    for (int q = 0; q < BT_VECS; ++q) {
+    for (int q = 0; q < V; ++q) {
       for (int o = 32; o > 0; o >>= 1) s[q] += __shfl_xor(s[q], o);
       if ((tid & 63) == 0) red[q][tid >> 6] = s[q];
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < BT_VECS; ++q) s[q] = t * ((red[q][0] + red[q][1]) + (red[q][2] + red[q][3]));
+    for (int q = 0; q < V; ++q) s[q] = t * ((red[q][0] + red[q][1]) + (red[q][2] + red[q][3]));
     for (int i = k + 1 + tid; i < n; i += NTHREADS) {
       const double ui = u[i];
 #pragma unroll
-      for (int q = 0; q < BT_VECS; ++q) vs[q * n + i] -= s[q] * ui;
+      for (int q = 0; q < V; ++q) vs(q, i) -= s[q] * ui;
     }
     __syncthreads();
   }
   for (int i = tid; i < n; i += NTHREADS)
-    for (int q = 0; q < nv; ++q) evecs[(int64_t)i * ldv + j0 + q] = (float)vs[q * n + i];
+    for (int q = 0; q < nv; ++q) evecs[(int64_t)i * ldv + j0 + q] = (float)vs(q, i);
 }
 
 // n > EIG_LDS_MAX: tridiagonalisation plan (grid, rows per workgroup, row storage).
@@ -835,6 +856,7 @@ __global__ __launch_bounds__(NTHREADS) void eig_backtransform(const double* U, c
 struct TriPlan {
   int G, R, RB;  // workgroups, rows per workgroup, rows per row-pass batch
   bool lds_rows;
+  bool vec_lds;  // the 3n vector doubles fit LDS (n <= 6400); else a global slab per workgroup
   size_t shmem, ws;
 };
 constexpr size_t TRI_LDS_BUDGET = 150 * 1024;
@@ -851,9 +873,13 @@ static size_t tri_zero_bytes(int n) {
 
 static TriPlan tri_plan(int n, bool vecs) {
   TriPlan p;
-  const size_t vec = (size_t)3 * n * sizeof(double);
+  const size_t vec_bytes = (size_t)3 * n * sizeof(double);
+  p.vec_lds = vec_bytes <= TRI_LDS_BUDGET;
+  const size_t vec = p.vec_lds ? vec_bytes : 0;
   const size_t row = (size_t)n * sizeof(double);
-  const int rmax = vec < TRI_LDS_BUDGET ? (int)((TRI_LDS_BUDGET - vec) / row) : 0;
+  // vectors in global memory (n > 6400) leave at most 2 rows per workgroup of LDS: the
+  // rows go to the global slab too
+  const int rmax = p.vec_lds && vec < TRI_LDS_BUDGET ? (int)((TRI_LDS_BUDGET - vec) / row) : 0;
   const int gmin = rmax > 0 ? (n + rmax - 1) / rmax : 1 << 30;
   p.lds_rows = gmin <= 256;
   if (p.lds_rows) {
@@ -874,6 +900,7 @@ static TriPlan tri_plan(int n, bool vecs) {
   p.ws = tri_zero_bytes(n)                                       // abort + granules
          + 2 * align_up((size_t)n * sizeof(double), 256)         // d, e
          + (p.lds_rows ? 0 : align_up((size_t)p.G * p.R * n * sizeof(double), 256))
+         + (p.vec_lds ? 0 : align_up((size_t)p.G * 3 * n * sizeof(double), 256))
          + (vecs ? 2 * align_up((size_t)n * n * sizeof(double), 256)  // U, Z
                        + 5 * align_up((size_t)n * cdiv(n, NTHREADS) * NTHREADS * sizeof(double), 256)
                        + align_up((size_t)n * sizeof(double), 256)    // tau
@@ -884,7 +911,7 @@ static TriPlan tri_plan(int n, bool vecs) {
 static int tridiag_eig(const kfac_eig_job& j, char* ws, int32_t* info, hipStream_t stream) {
   const bool vecs = j.evecs != nullptr;
   const TriPlan pl = tri_plan(j.n, vecs);
-  if (pl.shmem > TRI_LDS_BUDGET) return KFAC_EINVAL;
+  if (pl.shmem > TRI_LDS_BUDGET) return KFAC_EINVAL;  // unreachable: vectors / rows fall back
   TriArgs t{};
   t.F = j.F; t.ldF = j.ldF; t.n = j.n; t.G = pl.G; t.R = pl.R;
   t.abort = reinterpret_cast<unsigned*>(ws);
@@ -894,6 +921,8 @@ static int tridiag_eig(const kfac_eig_job& j, char* ws, int32_t* info, hipStream
   t.e = reinterpret_cast<double*>(q); q += align_up((size_t)j.n * sizeof(double), 256);
   t.rows_g = pl.lds_rows ? nullptr : reinterpret_cast<double*>(q);
   if (!pl.lds_rows) q += align_up((size_t)pl.G * pl.R * j.n * sizeof(double), 256);
+  t.vecs_g = pl.vec_lds ? nullptr : reinterpret_cast<double*>(q);
+  if (!pl.vec_lds) q += align_up((size_t)pl.G * 3 * j.n * sizeof(double), 256);
   double *Z = nullptr, *scratch = nullptr;
   if (vecs) {
     const size_t nn = align_up((size_t)j.n * j.n * sizeof(double), 256);
@@ -908,10 +937,11 @@ static int tridiag_eig(const kfac_eig_job& j, char* ws, int32_t* info, hipStream
   // abort word and every granule start at zero (tag 0 never matches an epoch)
   if (hipMemsetAsync(ws, 0, tri_zero_bytes(j.n), stream) != hipSuccess) return KFAC_ELAUNCH;
   const bool rb8 = pl.RB == 8;
-  const void* fn = pl.lds_rows ? (rb8 ? reinterpret_cast<const void*>(&eig_tridiag<true, 8>)
-                                      : reinterpret_cast<const void*>(&eig_tridiag<true, 4>))
-                               : (rb8 ? reinterpret_cast<const void*>(&eig_tridiag<false, 8>)
-                                      : reinterpret_cast<const void*>(&eig_tridiag<false, 4>));
+  const void* fn = !pl.vec_lds ? reinterpret_cast<const void*>(&eig_tridiag<false, 4, false>)
+                  : pl.lds_rows ? (rb8 ? reinterpret_cast<const void*>(&eig_tridiag<true, 8>)
+                                       : reinterpret_cast<const void*>(&eig_tridiag<true, 4>))
+                                : (rb8 ? reinterpret_cast<const void*>(&eig_tridiag<false, 8>)
+                                       : reinterpret_cast<const void*>(&eig_tridiag<false, 4>));
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.shmem) != hipSuccess)
     return KFAC_ELAUNCH;
   static uint64_t* prof = nullptr;  // debug: step-phase stamps (KFAC_EIG_PROF=1; synchronises)
@@ -946,26 +976,48 @@ static int tridiag_eig(const kfac_eig_job& j, char* ws, int32_t* info, hipStream
             ph[0] / steps / 100.0, ph[1] / steps / 100.0, ph[2] / steps / 100.0, ph[3] / steps / 100.0,
             ph[4] / steps / 100.0, (double)(h[(size_t)(steps - 1) * 5 + 4] - h[0]) / 1e5);
   }
-  // one wave per eigenvalue; d and e^2 in LDS (2 n doubles <= 64 KiB up to n = 4096)
-  const size_t bsh = (size_t)2 * j.n * sizeof(double);
-  if (bsh > TRI_LDS_BUDGET) return KFAC_EINVAL;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&eig_bisect),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)bsh) != hipSuccess)
+  // one wave per eigenvalue; d and e^2 in LDS while 2 n doubles fit (n <= 9600), else
+  // read from global memory
+  const size_t bsh2 = (size_t)2 * j.n * sizeof(double);
+  const bool bsh_lds = bsh2 <= TRI_LDS_BUDGET;
+  const size_t bsh = bsh_lds ? bsh2 : 0;
+  const void* bfn = bsh_lds ? reinterpret_cast<const void*>(&eig_bisect<true>)
+                            : reinterpret_cast<const void*>(&eig_bisect<false>);
+  if (hipFuncSetAttribute(bfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bsh) != hipSuccess)
     return KFAC_ELAUNCH;
-  hipLaunchKernelGGL(eig_bisect, dim3((j.n + NTHREADS / 64 - 1) / (NTHREADS / 64)), dim3(NTHREADS), bsh,
-                     stream, t.d, t.e, j.n, j.evals, t.abort, info);
+  if (bsh_lds)
+    hipLaunchKernelGGL(eig_bisect<true>, dim3((j.n + NTHREADS / 64 - 1) / (NTHREADS / 64)), dim3(NTHREADS),
+                       bsh, stream, t.d, t.e, j.n, j.evals, t.abort, info);
+  else
+    hipLaunchKernelGGL(eig_bisect<false>, dim3((j.n + NTHREADS / 64 - 1) / (NTHREADS / 64)), dim3(NTHREADS),
+                       0, stream, t.d, t.e, j.n, j.evals, t.abort, info);
   KFAC_CHECK_LAUNCH();
   if (vecs) {
     hipLaunchKernelGGL(eig_tri_vectors, dim3((j.n + NTHREADS - 1) / NTHREADS), dim3(NTHREADS), 0,
                        stream, t.d, t.e, j.evals, j.n, Z, scratch);
     KFAC_CHECK_LAUNCH();
-    const size_t sh = (size_t)BT_VECS * j.n * sizeof(double);
-    if (sh > TRI_LDS_BUDGET) return KFAC_EINVAL;
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&eig_backtransform),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh) != hipSuccess)
+    const size_t col = (size_t)j.n * sizeof(double);
+    const int V = 4 * col <= TRI_LDS_BUDGET ? 4 : 2 * col <= TRI_LDS_BUDGET ? 2 : col <= TRI_LDS_BUDGET ? 1 : 0;
+    const size_t sh = (size_t)V * col;
+    const void* bt = V == 4 ? reinterpret_cast<const void*>(&eig_backtransform<4, true>)
+                     : V == 2 ? reinterpret_cast<const void*>(&eig_backtransform<2, true>)
+                     : V == 1 ? reinterpret_cast<const void*>(&eig_backtransform<1, true>)
+                              : reinterpret_cast<const void*>(&eig_backtransform<1, false>);
+    if (hipFuncSetAttribute(bt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh) != hipSuccess)
       return KFAC_ELAUNCH;
-    hipLaunchKernelGGL(eig_backtransform, dim3((j.n + BT_VECS - 1) / BT_VECS), dim3(NTHREADS), sh,
-                       stream, t.U, t.tau, Z, j.n, j.evecs, j.ldv);
+    const dim3 bg((j.n + std::max(V, 1) - 1) / std::max(V, 1));
+    if (V == 4)
+      hipLaunchKernelGGL((eig_backtransform<4, true>), bg, dim3(NTHREADS), sh, stream, t.U, t.tau, Z, j.n,
+                         j.evecs, j.ldv);
+    else if (V == 2)
+      hipLaunchKernelGGL((eig_backtransform<2, true>), bg, dim3(NTHREADS), sh, stream, t.U, t.tau, Z, j.n,
+                         j.evecs, j.ldv);
+    else if (V == 1)
+      hipLaunchKernelGGL((eig_backtransform<1, true>), bg, dim3(NTHREADS), sh, stream, t.U, t.tau, Z, j.n,
+                         j.evecs, j.ldv);
+    else
+      hipLaunchKernelGGL((eig_backtransform<1, false>), bg, dim3(NTHREADS), 0, stream, t.U, t.tau, Z, j.n,
+                         j.evecs, j.ldv);
     KFAC_CHECK_LAUNCH();
   }
   return KFAC_OK;

@@ -1324,25 +1324,29 @@ static bool job_glds(const kfac_factor_job& jb) {
 
 // bf16x3 SYRK (kfac_factor_syrk3) for a row-major launch group: every job either
 // LDS-eligible (16-byte rows, n > 32) or narrow (n <= 32, direct loads).
-// KFAC_SYRK3=1 selects it (default: the fp32-MFMA kernel until it wins the A/B).
-static bool syrk3_enabled() {
-  static const bool on = [] {
+// Default: a group whose largest factor has n >= 2048 (measured A/B, same box: wide
+// MLP 4097^2 factors 1.065e6 vs 9.37e5 img/s; the MNIST MLP's n <= 785 8.95e7 vs
+// 9.10e7 -- there the 28 macro tiles of a 785 factor leave the chip a quarter full
+// and the fp32 kernel's four workgroups per CU win).  KFAC_SYRK3=1 / 0 forces it.
+static int syrk3_mode() {
+  static const int m = [] {
     const char* v = getenv("KFAC_SYRK3");
-    return v && v[0] == '1';
+    return v && v[0] == '1' ? 1 : v && v[0] == '0' ? 0 : -1;
   }();
-  return on;
+  return m;
 }
 
 static bool syrk3_group(const kfac_factor_job* jobs, int njobs) {
-  if (!syrk3_enabled() || njobs <= 0) return false;
-  bool big = false;
+  const int mode = syrk3_mode();
+  if (mode == 0 || njobs <= 0) return false;
+  int nmax = 0;
   for (int i = 0; i < njobs; ++i) {
     if (jobs[i].x.layout != KFAC_ROWMAJOR) return false;
     const int n = factor_n(jobs[i]);
     if (n > 32 && !job_glds(jobs[i])) return false;
-    big |= n > 32;
+    nmax = std::max(nmax, n);
   }
-  return big;
+  return nmax > 32 && (mode == 1 || nmax >= 2048);
 }
 
 static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
@@ -1533,8 +1537,9 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
   FactorArgs& red = g.red;
   const int tasks = g.tasks, rtiles = g.rtiles;
   if (tasks == 0) return KFAC_OK;
+  const bool s3 = syrk3_group(jobs, njobs);
   {
-    ProfScope ps(KFAC_PROF_FACTOR_TILES, stream);
+    ProfScope ps(s3 ? KFAC_PROF_FACTOR_SYRK3 : KFAC_PROF_FACTOR_TILES, stream);
     // launch_groups() gives every channel-major / im2col job a group of its own
     // conv jobs whose images fit LDS: the image-staged kernel
     ConvGeom cg;
@@ -1556,7 +1561,7 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
         {
           bool all_glds = true;
           for (int i = 0; i < njobs; ++i) all_glds &= args.job[i].glds != 0 || args.job[i].n <= 32;
-          if (syrk3_group(jobs, njobs)) {
+          if (s3) {
             static const bool attr = hipFuncSetAttribute(
                 reinterpret_cast<const void*>(&kfac_factor_syrk3),
                 hipFuncAttributeMaxDynamicSharedMemorySize, S3_LDS) == hipSuccess;

@@ -48,15 +48,21 @@ def main(tag):
         stats[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3}
     with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
         json.dump(pmc, f, indent=1, sort_keys=True)
-    t = pmc.get("kfac_factor_tiles", {})
+    # the dominant factor kernel of the run: the bf16x3 SYRK when it ran (wide), else
+    # the fp32-MFMA one
+    kname = "kfac_factor_syrk3" if "FETCH_SIZE" in pmc.get("kfac_factor_syrk3", {}) else "kfac_factor_tiles"
+    t = pmc.get(kname, {})
     if "FETCH_SIZE" in t and "WRITE_SIZE" in t:
         fetch = t["FETCH_SIZE"]["mean_per_dispatch"] * 1024 * 2  # gfx950: x2 for 16 B/lane reads
         write = t["WRITE_SIZE"]["mean_per_dispatch"] * 1024
-        out = {"kernel": "kfac_factor_tiles", "tag": tag, "fetch_bytes_per_launch": fetch,
+        note = ("FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->bytes, "
+                "mean over the bench's launches (15 updates per pass, last batch short)")
+        if kname == "kfac_factor_syrk3":
+            note += ("; syrk3's panel loads are 4 B/lane buffer loads, for which the x2 is "
+                     "uncalibrated (MI355X_MICROARCH.md): fetch is an upper bound, x1 the lower")
+        out = {"kernel": kname, "tag": tag, "fetch_bytes_per_launch": fetch,
                "write_bytes_per_launch": write, "hbm_bytes_per_launch": fetch + write,
-               "rocprof_trace": stats.get("kfac_factor_tiles"),
-               "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->bytes, "
-                       "mean over the bench's launches (15 updates per pass, last batch short)"}
+               "rocprof_trace": stats.get(kname), "note": note}
         with open(os.path.join(dst, "factor_tiles_hbm.json"), "w") as f:
             json.dump(out, f, indent=1)
         # the files bench.py reads: factor_tiles_pmc.json for the headline (MLP) profile,
