@@ -444,15 +444,17 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
 //
 // Work unit: one 128 x 128 macro tile (= 2 x 2 of the 64-tiles whose partial slabs
 // the reduce sums) of one factor over one K-chunk; one workgroup per CU (96 KB of
-// LDS), 512 threads in two roles, one of each per SIMD:
+// LDS), 768 threads in two roles, one consumer and two producers per SIMD:
 //   consumers (waves 0-3): wave w computes the 64 x 64 quadrant (w >> 1, w & 1) =
 //     2 x 2 blocks of 32 x 32 -- fragment reads and MFMAs only;
-//   producers (waves 4-7): load the next stage's rows, split them into the three
-//     bf16 parts and store them -- global loads, VALU and LDS stores only,
-// so each SIMD's MFMA pipe is fed by one wave while the other does the conversion
-// work beside it; one barrier per stage hands the stage over (double-buffered).
-// A stage = 32 rows of K; a producer thread takes 8 rows of 2 columns of the A
-// panel and the same of the B panel.  LDS image per stage: two substep regions
+//   producers (waves 4-11; 4-7 the A panel, 8-11 the B panel): load the next
+//     stage's rows, split them into the three bf16 parts and store them -- global
+//     loads, VALU and LDS stores only,
+// so each SIMD's MFMA pipe is fed by one wave while two others do the conversion
+// work beside it (one producer wave per SIMD measured as the critical path: the
+// kernel took 88 % as long with the MFMAs removed); one barrier per stage hands the
+// stage over (double-buffered).  A stage = 32 rows of K; a producer thread takes 8
+// rows of 2 columns of its panel.  LDS image per stage: two substep regions
 // (k 0-15, 16-31), each [part][column][2 chunks of 8 k] (32 B per column, k
 // contiguous), read straight into MFMA operands (lane = column, 8 k per
 // ds_read_b128).  The chunk of a column is XOR-swizzled by bit 3 of the column and
@@ -460,7 +462,7 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
 // both conflict-free, and every fragment read is a per-lane base plus an immediate.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int MT = 128;                          // macro tile edge
-constexpr int S3_THREADS = 512;
+constexpr int S3_THREADS = 768;
 constexpr int S3_PART = 2 * MT * 32;             // bytes of one part of one substep region
 constexpr int S3_REG = 3 * S3_PART + 64;         // substep region (+64: store banks)
 constexpr int S3_STAGE = 2 * S3_REG;
@@ -494,26 +496,49 @@ __device__ __forceinline__ void split3(float a, float b, uint32_t& h, uint32_t& 
   l = bf16_pair(sa, sb);
 }
 
-// A producer thread's share of a stage: rows 8q .. 8q+7 of columns (panel 0: A,
-// 1: B) 4g + e and 4g + e + 2.  S3_DEPTH stages of loads are in flight (register
-// ring): the rows come from L2 / the Infinity Cache, ~1 us away, and a stage
-// computes in about that.
+// A producer thread's share of a stage: rows 8q .. 8q+7 of the column pair 2g, 2g+1
+// of its panel (one 8-byte load per row).  S3_DEPTH stages of loads are in flight
+// (register ring).  Its stores put both columns' 8 k of a part in two 16-byte
+// chunks: the 8 lanes of a ds_write_b128 group hit 4 distinct bank groups twice
+// (2-way; the 2-column-apart mapping that avoided it needed twice the loads).
 constexpr int S3_DEPTH = 3;
 struct S3Prod {
-  int vob[2][8];      // byte offset of row 8q + r of the panel's first column (OOB: fill)
-  float fill[2];      // 1 for the bias ones column, else 0 (first column of a panel)
-  int off0, off1;     // LDS byte offsets of the two columns' chunks (A panel; B: + 128 columns)
+  int vob[8];       // byte offset of row 8q + r of the pair (OOB: a fill pair)
+  uint32_t hfill;   // the bias ones column's hi part (bf16 1.0 pair) on its lanes, else 0
+  int off0, off1;   // LDS byte offsets of the two columns' chunks in a stage
   int q;
 };
-typedef float S3Rows[2][2][8];  // [panel][column][row] of one stage
+typedef float S3Rows[2][8];  // [column][row] of one stage
 
-// loads of the stage at `cur` into v: raw buffer loads of the stage's rows (base and
-// size uniform, from SGPRs) at per-thread byte offsets; rows past the batch and fill
-// columns fall outside the buffer and read 0; the ones column adds its 1.
-template <int NP>
-__device__ __forceinline__ void s3_load(const S3Prod& P, S3Rows& v, const FactorJobDev& J,
-                                        const float* const* segs, StageCursor& cur, int ld) {
-  const uint64_t bpu = reinterpret_cast<uint64_t>(seg_base(J, segs, cur.seg) + cur.k * ld);
+// The producer's stage cursor: the stage's first row as a uniform base pointer,
+// advanced by 32 rows per stage (a new batch base at a batch boundary).
+struct S3Cur {
+  const float* bp;
+  int64_t k;
+  int seg;
+  __device__ __forceinline__ void init(const FactorJobDev& J, const float* const* segs, int64_t s, int ld) {
+    seg = (int)(s / J.sps);
+    k = (s - (int64_t)seg * J.sps) * BK;
+    bp = seg_base(J, segs, seg) + k * ld;
+  }
+  __device__ __forceinline__ void next(const FactorJobDev& J, const float* const* segs, int ld) {
+    k += BK;
+    bp += (int64_t)BK * ld;
+    if (k >= J.x.rows) {
+      k = 0;
+      ++seg;
+      bp = seg_base(J, segs, seg);
+    }
+  }
+};
+
+// loads of the stage at `cur` into v (returns its real rows): raw buffer loads of
+// the stage's rows (base and size uniform, from SGPRs) at per-thread byte offsets;
+// rows past the batch and fill columns fall outside the buffer and read 0 (the ones
+// column gets its 1 at the commit)
+__device__ __forceinline__ int s3_load(const S3Prod& P, S3Rows& v, const FactorJobDev& J,
+                                       const float* const* segs, S3Cur& cur, int ld) {
+  const uint64_t bpu = reinterpret_cast<uint64_t>(cur.bp);
   // (uniform by construction; readfirstlane tells the compiler, else it wraps every
   // buffer load in a waterfall loop.  readfirstlane returns int: zero-extend)
   void* bp = reinterpret_cast<void*>(
@@ -523,38 +548,67 @@ __device__ __forceinline__ void s3_load(const S3Prod& P, S3Rows& v, const Factor
   const int nrow = __builtin_amdgcn_readfirstlane(left < BK ? (int)left : BK);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       bp, (short)0, __builtin_amdgcn_readfirstlane(nrow * ld * 4), 0x00020000);
+  typedef float float2v __attribute__((ext_vector_type(2)));
 #pragma unroll
-  for (int pn = 0; pn < NP; ++pn)
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      v[pn][0][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, P.vob[pn][r], 0, 0));
-      v[pn][1][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, P.vob[pn][r] + 8, 0, 0));
-    }
-  // the ones column: 1 on the stage's real rows (added once the loads have landed:
-  // the values are kept as an offset until the commit)
-  (void)nrow;
-  cur.next(J.x.rows);
+  for (int r = 0; r < 8; ++r) {
+    const float2v x = __builtin_bit_cast(float2v, __builtin_amdgcn_raw_buffer_load_b64(rs, P.vob[r], 0, 0));
+    v[0][r] = x[0];
+    v[1][r] = x[1];
+  }
+  cur.next(J, segs, ld);
+  return nrow;
 }
 
-// v -> hi / mid / lo parts -> the thread's chunks of a stage (`nrow` real rows)
-template <int NP>
+// v -> hi / mid / lo parts -> the thread's chunks of a stage (`nrow` real rows).  The
+// 8 pair-splits run step by step side by side (independent chains between the
+// conversions, which need wait states before their results are read); the ones
+// column's 1.0 is OR-ed into its hi part (its loads read 0).
 __device__ __forceinline__ void s3_commit(const S3Prod& P, S3Rows& v, int nrow, char* stage) {
+  uint32_t h[2][4], m[2][4], l[2][4];
+  float ra[2][4], rb[2][4];
 #pragma unroll
-  for (int pn = 0; pn < NP; ++pn)
+  for (int c = 0; c < 2; ++c)
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[pn][0][r] += (8 * P.q + r < nrow) ? P.fill[pn] : 0.f;
+    for (int i = 0; i < 4; ++i) h[c][i] = bf16_pair(v[c][2 * i], v[c][2 * i + 1]);
 #pragma unroll
-  for (int pn = 0; pn < NP; ++pn)
+  for (int c = 0; c < 2; ++c)
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      uint32_t h[4], m[4], l[4];
-#pragma unroll
-      for (int r2 = 0; r2 < 4; ++r2) split3(v[pn][c][2 * r2], v[pn][c][2 * r2 + 1], h[r2], m[r2], l[r2]);
-      char* d = stage + (c ? P.off1 : P.off0) + pn * MT * 32;
-      *reinterpret_cast<uint4*>(d) = make_uint4(h[0], h[1], h[2], h[3]);
-      *reinterpret_cast<uint4*>(d + S3_PART) = make_uint4(m[0], m[1], m[2], m[3]);
-      *reinterpret_cast<uint4*>(d + 2 * S3_PART) = make_uint4(l[0], l[1], l[2], l[3]);
+    for (int i = 0; i < 4; ++i) {
+      ra[c][i] = sub_f32(v[c][2 * i], __uint_as_float(h[c][i] << 16));
+      rb[c][i] = sub_f32(v[c][2 * i + 1], __uint_as_float(h[c][i] & 0xffff0000u));
     }
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m[c][i] = bf16_pair(ra[c][i], rb[c][i]);
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ra[c][i] = sub_f32(ra[c][i], __uint_as_float(m[c][i] << 16));
+      rb[c][i] = sub_f32(rb[c][i], __uint_as_float(m[c][i] & 0xffff0000u));
+    }
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) l[c][i] = bf16_pair(ra[c][i], rb[c][i]);
+  if (nrow == BK) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h[0][i] |= P.hfill;
+  } else {  // a partial stage: the ones column only on its real rows
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 8 * P.q + 2 * i;
+      h[0][i] |= P.hfill & ((r < nrow ? 0x0000ffffu : 0u) | (r + 1 < nrow ? 0xffff0000u : 0u));
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    char* d = stage + (c ? P.off1 : P.off0);
+    *reinterpret_cast<uint4*>(d) = make_uint4(h[c][0], h[c][1], h[c][2], h[c][3]);
+    *reinterpret_cast<uint4*>(d + S3_PART) = make_uint4(m[c][0], m[c][1], m[c][2], m[c][3]);
+    *reinterpret_cast<uint4*>(d + 2 * S3_PART) = make_uint4(l[c][0], l[c][1], l[c][2], l[c][3]);
+  }
 }
 
 // A consumer wave's MFMAs on one stage: blocks (bi, bj) of its 64 x 64 quadrant with
@@ -563,31 +617,42 @@ __device__ __forceinline__ void s3_commit(const S3Prod& P, S3Rows& v, int nrow, 
 __device__ __forceinline__ void s3_consume(const char* stage, int oa, int ob, const bool (&act)[2][2],
                                            floatx16 (&acc)[2][2]) {
   auto frag = [&](int off) { return *reinterpret_cast<const bf16x8*>(stage + off); };
-  bf16x8 a[2][2][3], b[2][2][3];  // [substep][block][part]
+  auto six = [&](int bi, int bj, const bf16x8* A, const bf16x8* B) {
+    if (!act[bi][bj]) return;
+    acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], acc[bi][bj], 0, 0, 0);
+    acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[1], acc[bi][bj], 0, 0, 0);
+    acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[2], acc[bi][bj], 0, 0, 0);
+    acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0], acc[bi][bj], 0, 0, 0);
+    acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], acc[bi][bj], 0, 0, 0);
+    acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], acc[bi][bj], 0, 0, 0);
+  };
+  // fragments are read in the order they die, so at most 15 are live (60 VGPRs: with
+  // all 24 of a stage live the 768-thread workgroup filled the SIMDs' register files
+  // and the overlapped inversion's workgroups could not start beside it)
+  bf16x8 a0[3], a1[3], b0[3], b1[3];
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+  for (int p = 0; p < 3; ++p) {
+    a0[p] = frag(oa + p * S3_PART);
+    b0[p] = frag(ob + p * S3_PART);
+    b1[p] = frag(ob + p * S3_PART + 32 * 32);
+    a1[p] = frag(oa + p * S3_PART + 32 * 32);
+  }
+  six(0, 0, a0, b0);
+  six(0, 1, a0, b1);
 #pragma unroll
-    for (int x = 0; x < 2; ++x)
+  for (int p = 0; p < 3; ++p) a0[p] = frag(oa + S3_REG + p * S3_PART);
+  six(1, 0, a1, b0);
+  six(1, 1, a1, b1);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        a[s][x][p] = frag(oa + s * S3_REG + p * S3_PART + x * 32 * 32);
-        b[s][x][p] = frag(ob + s * S3_REG + p * S3_PART + x * 32 * 32);
-      }
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-      for (int bj = 0; bj < 2; ++bj) {
-        if (!act[bi][bj]) continue;
-        const bf16x8 *A = a[s][bi], *B = b[s][bj];
-        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], acc[bi][bj], 0, 0, 0);
-        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[1], acc[bi][bj], 0, 0, 0);
-        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[2], acc[bi][bj], 0, 0, 0);
-        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0], acc[bi][bj], 0, 0, 0);
-        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], acc[bi][bj], 0, 0, 0);
-        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], acc[bi][bj], 0, 0, 0);
-      }
+  for (int p = 0; p < 3; ++p) {
+    b0[p] = frag(ob + S3_REG + p * S3_PART);
+    b1[p] = frag(ob + S3_REG + p * S3_PART + 32 * 32);
+    a1[p] = frag(oa + S3_REG + p * S3_PART + 32 * 32);
+  }
+  six(0, 0, a0, b0);
+  six(0, 1, a0, b1);
+  six(1, 0, a1, b0);
+  six(1, 1, a1, b1);
 }
 
 // Macro tile of a unit index, in blocks of 4 tile rows x 8 tile columns of the lower
@@ -634,6 +699,9 @@ __device__ __forceinline__ void s3_task(const FactorJobDev& J, const float* cons
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (wave < 4) {
     // ---------------------------------------------------------------- consumer
+    // issue priority over the two producer waves on the SIMD: an MFMA that is ready
+    // goes first, the producers' VALU work fills the MFMA's shadow
+    __builtin_amdgcn_s_setprio(2);
     const int wr = wave >> 1, wc = wave & 1;
     bool act[2][2];
 #pragma unroll
@@ -676,63 +744,51 @@ __device__ __forceinline__ void s3_task(const FactorJobDev& J, const float* cons
   }
   // ---------------------------------------------------------------- producer
   if (ns <= 0) return;
-  // thread p -> row chunk q = p & 3 and columns 4g + e, 4g + e + 2 (g = p >> 3, e = (p >> 2) & 1)
-  // of each panel: the 8 lanes of a ds_write_b128 group cover both column parities x
-  // 4 chunks (conflict-free stores).  A diagonal tile loads its one panel.
-  const int p = tid - 256, q = p & 3, g = p >> 3, e = (p >> 2) & 1;
+  // thread p of panel pn -> row chunk q = p & 3 and the column pair 2g, 2g + 1 (g = p >> 2).
+  // A diagonal tile has one panel: the B-panel waves only meet the barriers.
+  const int pn = (tid - 256) >> 8, p = tid & 255, q = p & 3, g = p >> 2;
+  const bool works = pn == 0 || !same;  // wave-uniform
   const int ld = __builtin_amdgcn_readfirstlane((int)J.x.ld);  // (< 2^24: a stage's offsets fit 32 bits)
   S3Prod P;
   P.q = q;
-  P.off0 = (q >> 1) * S3_REG + s3_half(4 * g + e, q & 1);
-  P.off1 = (q >> 1) * S3_REG + s3_half(4 * g + e + 2, q & 1);
+  P.off0 = (q >> 1) * S3_REG + s3_half(pn * MT + 2 * g, q & 1);
+  P.off1 = (q >> 1) * S3_REG + s3_half(pn * MT + 2 * g + 1, q & 1);
+  {
+    const int col = (pn ? Jc : I) * MT + 2 * g;
+    const bool real = col < J.x.cols;  // cols % 4 == 0: a pair is all real or all fill
+    P.hfill = (col == J.x.ones) ? 0x3f803f80u : 0u;  // bf16 (1.0, 1.0)
 #pragma unroll
-  for (int pn = 0; pn < 2; ++pn) {
-    const int col = (pn ? Jc : I) * MT + 4 * g + e;
-    const bool real = col < J.x.cols;  // cols % 4 == 0: a 4-column group is all real or all fill
-    P.fill[pn] = (col == J.x.ones) ? 1.f : 0.f;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) P.vob[pn][r] = real ? ((8 * q + r) * ld + col) * 4 : 0x7fffff00;
+    for (int r = 0; r < 8; ++r) P.vob[r] = real ? ((8 * q + r) * ld + col) * 4 : 0x7fffff00;
   }
-  StageCursor cur;
-  cur.init(J, s0);
-  // real rows of stage i (its loads are in flight until its commit): the ring's
-  // stages are consecutive, so they are tracked with a second cursor
-  StageCursor rc = cur;
-  auto rows_of = [&]() {
-    const int64_t left = J.x.rows - rc.k;
-    const int nrow = __builtin_amdgcn_readfirstlane(left < BK ? (int)left : BK);
-    rc.next(J.x.rows);
-    return nrow;
-  };
-  auto run = [&](auto npc) {
-    constexpr int NP = decltype(npc)::value;
-    S3Rows v[S3_DEPTH];
-    // stage i lives in ring slot i % S3_DEPTH; the loop is unrolled by the ring depth
-    // so every slot is a fixed register set
+  if (!works) {
+    for (int st = 0; st <= ns; ++st) __syncthreads();
+    return;
+  }
+  S3Cur cur;
+  cur.init(J, segs, s0, ld);
+  S3Rows v[S3_DEPTH];
+  int nr[S3_DEPTH];  // real rows of the stage in each ring slot
+  // stage i lives in ring slot i % S3_DEPTH; the loop is unrolled by the ring depth
+  // so every slot is a fixed register set
 #pragma unroll
-    for (int i = 0; i < S3_DEPTH; ++i)
-      if (i < ns) s3_load<NP>(P, v[i], J, segs, cur, ld);
-    s3_commit<NP>(P, v[0], rows_of(), lds);
-    if (S3_DEPTH < ns) s3_load<NP>(P, v[0], J, segs, cur, ld);
-    __syncthreads();  // stage 0 stored
-    for (int st0 = 0; st0 < ns; st0 += S3_DEPTH) {
+  for (int i = 0; i < S3_DEPTH; ++i)
+    if (i < ns) nr[i] = s3_load(P, v[i], J, segs, cur, ld);
+  s3_commit(P, v[0], nr[0], lds);
+  if (S3_DEPTH < ns) nr[0] = s3_load(P, v[0], J, segs, cur, ld);
+  __syncthreads();  // stage 0 stored
+  for (int st0 = 0; st0 < ns; st0 += S3_DEPTH) {
 #pragma unroll
-      for (int u = 0; u < S3_DEPTH; ++u) {
-        const int st = st0 + u;  // consumers compute stage st; store stage st+1
-        if (st >= ns) break;
-        if (st + 1 < ns) {
-          constexpr int dummy = 0;
-          (void)dummy;
-          S3Rows& nx = v[(u + 1) % S3_DEPTH];
-          s3_commit<NP>(P, nx, rows_of(), lds + ((st + 1) & 1) * S3_STAGE);
-          if (st + 1 + S3_DEPTH < ns) s3_load<NP>(P, nx, J, segs, cur, ld);
-        }
-        __syncthreads();
+    for (int u = 0; u < S3_DEPTH; ++u) {
+      const int st = st0 + u;  // consumers compute stage st; store stage st+1
+      if (st >= ns) break;
+      if (st + 1 < ns) {
+        const int sl = (u + 1) % S3_DEPTH;  // (a constant once unrolled)
+        s3_commit(P, v[sl], nr[sl], lds + ((st + 1) & 1) * S3_STAGE);
+        if (st + 1 + S3_DEPTH < ns) nr[sl] = s3_load(P, v[sl], J, segs, cur, ld);
       }
+      __syncthreads();
     }
-  };
-  if (same) run(std::integral_constant<int, 1>{});
-  else run(std::integral_constant<int, 2>{});
+  }
 }
 
 __global__ __launch_bounds__(S3_THREADS, 1) void kfac_factor_syrk3(FactorArgs args) {
