@@ -838,7 +838,8 @@ struct ConvGeom {
   int mode;        // 0: 64x64 tiles, 1: narrow 32x32, 2: narrow 16x16
   int n;           // factor order
   int KR;          // k-lanes per MFMA (2 or 4)
-  int B;           // images of the batch
+  int B;           // images of the job: nseg batches x bseg images
+  int bseg;        // images per batch (a multi-batch job walks the queued batches' bases)
   int T;           // MFMAs along one row group (PATCH: Wo; CHANNEL: segment length Q)
   int G;           // row groups (PATCH: ceil(Ho / KR)); CHANNEL: 1
   int stride;      // LDS step between consecutive MFMAs (PATCH: sw; CHANNEL: 1)
@@ -893,7 +894,8 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args,
   using PreT = std::conditional_t<LAYOUT == KFAC_PATCH, float, floatx4>;
   PreT pre[PMAXE];
   auto fetch = [&](int64_t b) {
-    const float* src = op.ptr + b * op.sB;
+    const int seg = (int)((uint32_t)b / (uint32_t)cg.bseg);
+    const float* src = seg_base(J, args.segs, seg) + (b - (int64_t)seg * cg.bseg) * op.sB;
 #pragma unroll
     for (int q = 0; q < PMAXE; ++q) {
       if (dmap[q] < 0) continue;
@@ -1123,11 +1125,12 @@ __global__ __launch_bounds__(NTHREADS) void kfac_factor_channel_small(FactorArgs
   float acc[NT];
 #pragma unroll
   for (int e = 0; e < NT; ++e) acc[e] = 0.f;
-  const float* base = op.ptr + b0 * op.sB;
   int64_t img = tid / L4, r4 = tid - img * L4;
   const int64_t dimg = NTHREADS / L4, dr = NTHREADS - dimg * L4;
   for (int64_t q = tid; q < per; q += NTHREADS) {
-    const float* src = base + img * op.sB + 4 * r4;
+    // image b0 + img of the job: batch seg of the queued batches, image bi in it
+    const uint32_t ab = (uint32_t)(b0 + img), seg = ab / (uint32_t)cg.bseg;
+    const float* src = seg_base(J, args.segs, (int)seg) + (int64_t)(ab - seg * cg.bseg) * op.sB + 4 * r4;
     floatx4 x[NMAX];
 #pragma unroll
     for (int c = 0; c < NMAX; ++c) {
@@ -1183,19 +1186,21 @@ static bool conv_small_off() {
 }
 
 // Geometry of a conv job on the LDS-staged kernel; false: the job takes the
-// register-staged path (images too large, channel blocks not float4-shaped, a
-// multi-batch job, or an empty batch).
+// register-staged path (images too large, channel blocks not float4-shaped, or an
+// empty batch).  A multi-batch job's images are its nseg batches' images in order.
 static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
   const kfac_operand& o = j.x;
+  const int64_t nseg = j.nseg > 1 ? j.nseg : 1;
   if ((o.layout != KFAC_PATCH && o.layout != KFAC_CHANNEL) || o.rows <= 0 || o.L <= 0 ||
-      j.nseg > 1 || o.rows % o.L != 0 || o.rows / o.L > (1 << 30))
+      o.rows % o.L != 0 || nseg * (o.rows / o.L) > (1 << 30))
     return false;
   const int n = o.cols + (o.has_ones ? 1 : 0);
   g = ConvGeom{};
   g.n = n;
   g.mode = n <= 16 ? 2 : (n <= 32 ? 1 : 0);
   g.KR = g.mode == 2 ? 4 : 2;
-  g.B = (int)(o.rows / o.L);
+  g.bseg = (int)(o.rows / o.L);
+  g.B = (int)(nseg * g.bseg);
   int64_t lds;
   // Bank-conflict-free operand reads: an MFMA's 32 lanes of one lane group read 32
   // consecutive factor columns, column (c, ki, kj) at c*plane + ki*Wp + kj (PATCH) or
@@ -1692,8 +1697,7 @@ static int validate(const kfac_factor_job* jobs, int njobs) {
     if (!valid_operand(j.x) || !j.F || j.ldF < factor_n(j)) return KFAC_EINVAL;
     if ((int64_t)factor_n(j) > (int64_t)1 << 20) return KFAC_EINVAL;
     if (j.acc && (j.acc_splits <= 0 || j.acc_splits > (1 << 20))) return KFAC_EINVAL;
-    if (j.nseg < 0 || (j.nseg > 1 && (!j.seg_ptrs || j.x.layout != KFAC_ROWMAJOR)) ||
-        job_sps(j) > (1 << 30))
+    if (j.nseg < 0 || (j.nseg > 1 && !j.seg_ptrs) || job_sps(j) > (1 << 30))
       return KFAC_EINVAL;
   }
   return KFAC_OK;
@@ -1730,6 +1734,26 @@ extern "C" int kfac_factor_update(const kfac_factor_job* jobs, int njobs, void* 
   launch_groups(jobs, njobs, sorted, order, groups);
   for (const auto& g : groups) {
     const kfac_factor_job* gj = sorted.data() + g.first;
+    ConvGeom cg;
+    if (g.second == 1 && gj[0].x.layout != KFAC_ROWMAJOR && job_nseg(gj[0]) > 1 && !conv_geom(gj[0], cg)) {
+      // a multi-batch conv job off the image-staged kernel (images too large for LDS):
+      // the register-staged kernels read one batch base, so one launch per batch,
+      // each adding to what the previous one wrote
+      const float* const* bases = reinterpret_cast<const float* const*>(gj[0].seg_ptrs);
+      for (int s = 0; s < gj[0].nseg; ++s) {
+        kfac_factor_job j = gj[0];
+        j.seg_ptrs = nullptr;
+        j.nseg = 0;
+        j.x.ptr = bases[s];
+        if (s > 0) {
+          if (j.acc) j.acc_beta = 1.f;
+          else j.beta = 1.f;
+        }
+        const int rc = factor_group(&j, 1, (char*)workspace, workspace_bytes, (hipStream_t)stream);
+        if (rc != KFAC_OK) return rc;
+      }
+      continue;
+    }
     int multi = 0, maxseg = 1, total = 0;
     for (int k = 0; k < g.second; ++k)
       if (job_nseg(gj[k]) > 1) {

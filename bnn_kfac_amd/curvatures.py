@@ -498,9 +498,8 @@ class KFAC(Curvature):
 
     def _launch_queue(self):
         """Launch the queued updates: consecutive updates with the same job templates
-        and operand alignment become one multi-batch job per row-major factor
-        (channel-major / im2col jobs, already B*Ho*Wo rows of K each, stay one job
-        per batch)."""
+        and operand alignment become one multi-batch job per factor (row-major: K
+        walks the batches; Conv2d im2col / channel-major: the images walk them)."""
         queue, self._queue = self._queue, []
         self._queue_bytes = 0
         for _jobs, _ptrs, keep, versions, _dev, _key in queue:
@@ -521,7 +520,7 @@ class KFAC(Curvature):
             tmpl = group[0][0]
             jobs = []
             for k, t in enumerate(tmpl):
-                if len(group) > 1 and t.x.layout == N.ROWMAJOR:
+                if len(group) > 1:
                     job = N.FactorJob.from_buffer_copy(t)
                     job.x.ptr = group[0][1][k]
                     table = N.segment_table([e[1][k] for e in group])

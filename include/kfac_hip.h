@@ -91,8 +91,10 @@ typedef struct kfac_factor_job {
    * (K = nseg * x.rows, up to 64 bases per launch, more run as back-to-back
    * launches), so a pass of U equal batches costs about one MFMA launch instead
    * of U.  Equivalent to nseg jobs with the same alpha (the reference's per-batch
-   * mean over equal batches).  nseg 0 or 1 = the single batch at x.ptr.  nseg > 1
-   * needs KFAC_ROWMAJOR (a Conv2d batch is already B*Ho*Wo rows of K).        */
+   * mean over equal batches).  nseg 0 or 1 = the single batch at x.ptr.  Every
+   * layout: a KFAC_PATCH / KFAC_CHANNEL job's images are the nseg batches' B
+   * images each, in order (one launch per conv factor for the queued batches when
+   * an image fits the LDS-staged kernel; else one launch per batch).           */
   const void* seg_ptrs;
   int32_t nseg;
   int32_t reserved2;

@@ -339,3 +339,51 @@ def test_deferred_reduce_matches_immediate(hip_device, model):
     for other in outs[1:]:
         for got, want in zip(other, outs[0]):
             np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-6 * np.abs(want).max())
+
+
+@pytest.mark.parametrize("spec", [
+    # (B, Cin, H, W, Cout, k, stride, pad, bias): LeNet-5's conv1 / conv2 (n <= 8 channel
+    # kernel, staged im2col), a 32-wide channel factor with a narrow im2col one, and an
+    # image too large to stage (multi-batch job split into per-batch launches)
+    (64, 1, 28, 28, 6, (5, 5), (1, 1), (2, 2), True),
+    (32, 6, 14, 14, 16, (5, 5), (1, 1), (0, 0), True),
+    (4, 1, 10, 10, 20, (3, 3), (1, 1), (1, 1), True),
+    (2, 3, 40, 40, 5, (3, 3), (1, 1), (1, 1), True),
+])
+@pytest.mark.parametrize("deferred", [False, True])
+def test_conv_multibatch_queue_vs_oracle(hip_device, spec, deferred):
+    """Queued Conv2d updates become ONE multi-batch job per factor (the images walk
+    the batches' bases): 7 batches of separate allocations plus a short last one,
+    queued through KFAC.update, against the fp64 oracle's sum of per-batch means."""
+    from bnn_kfac_amd import _native as N
+    from bnn_kfac_amd.curvatures import KFAC
+    B, Cin, H, W, Cout, k, s, p, bias = spec
+    rng = np.random.default_rng(sum(spec[:5]) + 7)
+    conv = nn.Conv2d(Cin, Cout, k, stride=s, padding=p, bias=bias).to(hip_device)
+    Ho, Wo = (H + 2 * p[0] - k[0]) // s[0] + 1, (W + 2 * p[1] - k[1]) // s[1] + 1
+    sizes = [B] * 7 + [max(1, B // 3)]
+    xs = [rng.random((b, Cin, H, W), dtype=np.float32) for b in sizes]
+    gs = [rng.standard_normal((b, Cout, Ho, Wo), dtype=np.float32) for b in sizes]
+    kfac = KFAC(conv)
+    kfac.defer_reduce = deferred
+    kfac.launch_first = 8
+    calls = []
+    orig = N.factor_update
+
+    def counting(jobs, device):
+        calls.append([max(1, j.nseg) for j in jobs])
+        return orig(jobs, device)
+    N.factor_update = counting
+    try:
+        for x, g in zip(xs, gs):
+            kfac.record[conv] = [_t(x, hip_device), _t(g, hip_device)]
+            kfac.update(batch_size=x.shape[0])
+        A, G = kfac.state[conv]
+    finally:
+        N.factor_update = orig
+    if deferred:
+        assert calls[0] == [7, 7], calls  # the 7 equal batches: one job per factor
+    wA = sum(O.conv_factor_A(x, k, p, s, bias, np.float64) for x in xs)
+    wG = sum(O.grad_factor(g, np.float64) for g in gs)
+    np.testing.assert_allclose(A.cpu().numpy(), wA, **FT)
+    np.testing.assert_allclose(G.cpu().numpy(), wG, **FT)
