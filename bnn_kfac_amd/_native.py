@@ -62,6 +62,19 @@ class SampleJob(ctypes.Structure):
                 ("wcols", c_i32), ("dense", c_i32)]
 
 
+class EfbJob(ctypes.Structure):
+    _fields_ = [("VA", c_vp), ("ldA", c_i64), ("VG", c_vp), ("ldG", c_i64), ("grad", c_vp),
+                ("ld_grad", c_i64), ("state", c_vp), ("ld_state", c_i64), ("diag", c_vp),
+                ("ld_diag", c_i64), ("nA", c_i32), ("nG", c_i32), ("accumulate", c_i32),
+                ("scale", c_f32)]
+
+
+class GramJob(ctypes.Structure):
+    _fields_ = [("UA", c_vp), ("ldA", c_i64), ("UG", c_vp), ("ldG", c_i64), ("c", c_vp),
+                ("sigma", c_vp), ("out", c_vp), ("ldo", c_i64), ("nA", c_i32), ("nG", c_i32),
+                ("la", c_i32), ("lg", c_i32)]
+
+
 class TriJob(ctypes.Structure):
     _fields_ = [("F", c_vp), ("ldF", c_i64), ("n", c_i32), ("reserved", c_i32), ("offset", c_i64)]
 
@@ -98,6 +111,12 @@ SIGNATURES = {
     "kfac_sample_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(SampleJob), ctypes.c_int]),
     "kfac_sample": (ctypes.c_int, [ctypes.POINTER(SampleJob), ctypes.c_int, ctypes.c_int, c_vp,
                                    ctypes.c_size_t, c_vp]),
+    "kfac_efb_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(EfbJob), ctypes.c_int]),
+    "kfac_efb_update": (ctypes.c_int, [ctypes.POINTER(EfbJob), ctypes.c_int, c_vp, ctypes.c_size_t,
+                                       c_vp]),
+    "kfac_gram_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(GramJob), ctypes.c_int]),
+    "kfac_kron_gram": (ctypes.c_int, [ctypes.POINTER(GramJob), ctypes.c_int, c_vp, ctypes.c_size_t,
+                                      c_vp]),
     "kfac_tri_pack": (ctypes.c_int, [ctypes.POINTER(TriJob), ctypes.c_int, c_vp, c_vp]),
     "kfac_tri_unpack": (ctypes.c_int, [ctypes.POINTER(TriJob), ctypes.c_int, c_vp, ctypes.c_int, c_vp]),
     "kfac_profile_enable": (ctypes.c_int, [ctypes.c_int]),
@@ -292,6 +311,66 @@ def sample(jobs, device: torch.device, accumulate: bool) -> None:
         ws = workspace.get(device, L.kfac_sample_workspace_bytes(arr, len(chunk)))
         check(L.kfac_sample(arr, len(chunk), int(accumulate), ptr(ws), ws.numel(),
                             stream_handle(device)), "kfac_sample")
+
+
+def efb_update(jobs, device: torch.device) -> None:
+    """kfac_efb_update, <= 8 layers per launch pair (EFB.update)."""
+    L = lib()
+    for i in range(0, len(jobs), 8):
+        chunk = jobs[i:i + 8]
+        arr = as_array(EfbJob, chunk)
+        ws = workspace.get(device, L.kfac_efb_workspace_bytes(arr, len(chunk)))
+        check(L.kfac_efb_update(arr, len(chunk), ptr(ws), ws.numel(), stream_handle(device)),
+              "kfac_efb_update")
+
+
+def efb_job(VA: torch.Tensor, VG: torch.Tensor, grad: torch.Tensor, state: torch.Tensor,
+            diag, accumulate: bool, scale: float) -> EfbJob:
+    """One layer of EFB.update: state (+)= (VG^T grad VA)^2, diag (+)= grad^2 * scale."""
+    nG, nA = grad.shape
+    for t, what in ((VA, "V_A"), (VG, "V_G"), (grad, "grad"), (state, "state")):
+        require_device(t, what)
+        if t.dim() != 2 or t.stride(1) != 1:
+            raise ValueError(f"{what}: expected a 2-D tensor with unit column stride")
+    if tuple(VA.shape) != (nA, nA) or tuple(VG.shape) != (nG, nG) or tuple(state.shape) != (nG, nA):
+        raise ValueError(f"EFB shapes: V_A {tuple(VA.shape)}, V_G {tuple(VG.shape)}, grad "
+                         f"{tuple(grad.shape)}, state {tuple(state.shape)}")
+    j = EfbJob()
+    j.VA, j.ldA, j.VG, j.ldG = VA.data_ptr(), VA.stride(0), VG.data_ptr(), VG.stride(0)
+    j.grad, j.ld_grad = grad.data_ptr(), grad.stride(0)
+    j.state, j.ld_state = state.data_ptr(), state.stride(0)
+    if diag is not None:
+        require_device(diag, "diag")
+        if tuple(diag.shape) != (nG, nA) or diag.stride(1) != 1:
+            raise ValueError(f"diag: expected ({nG}, {nA}) row-major, got {tuple(diag.shape)}")
+        j.diag, j.ld_diag = diag.data_ptr(), diag.stride(0)
+    j.nA, j.nG, j.accumulate, j.scale = nA, nG, int(accumulate), float(scale)
+    return j
+
+
+def kron_gram(UA: torch.Tensor, UG: torch.Tensor, c: torch.Tensor, sigma: torch.Tensor) -> torch.Tensor:
+    """kfac_kron_gram: (la*lg)^2 = diag(sigma) V^T V diag(sigma), V = c * kron(UA, UG)
+    (INF.pre_sampler, curvatures.py:548-580), never forming V."""
+    for t, what in ((UA, "U_A"), (UG, "U_G"), (c, "correction"), (sigma, "sigma")):
+        require_device(t, what)
+    UA = UA if UA.stride(1) == 1 else UA.contiguous()
+    UG = UG if UG.stride(1) == 1 else UG.contiguous()
+    c, sigma = c.contiguous(), sigma.contiguous()
+    nA, la = UA.shape
+    nG, lg = UG.shape
+    if c.numel() != nA * nG or sigma.numel() != la * lg:
+        raise ValueError(f"kron_gram: c has {c.numel()} (want {nA * nG}), sigma {sigma.numel()} "
+                         f"(want {la * lg}) elements")
+    out = torch.empty(la * lg, la * lg, device=UA.device, dtype=torch.float32)
+    j = GramJob()
+    j.UA, j.ldA, j.UG, j.ldG = UA.data_ptr(), UA.stride(0), UG.data_ptr(), UG.stride(0)
+    j.c, j.sigma, j.out, j.ldo = c.data_ptr(), sigma.data_ptr(), out.data_ptr(), out.stride(0)
+    j.nA, j.nG, j.la, j.lg = nA, nG, la, lg
+    L = lib()
+    arr = as_array(GramJob, [j])
+    ws = workspace.get(UA.device, L.kfac_gram_workspace_bytes(arr, 1))
+    check(L.kfac_kron_gram(arr, 1, ptr(ws), ws.numel(), stream_handle(UA.device)), "kfac_kron_gram")
+    return out
 
 
 def sample_job(LA: torch.Tensor, LG: torch.Tensor, z: torch.Tensor, W: torch.Tensor, wcols: int,

@@ -813,7 +813,10 @@ class EFB(Curvature):
         self.diags = dict()
 
     def update(self, batch_size: int):
-        """curvatures.py:427-449: state += (V_G^T grad V_A)^2, diags += grad^2 * B."""
+        """curvatures.py:427-449: state += (V_G^T grad V_A)^2, diags += grad^2 * B --
+        every layer in one kfac_efb_update call (projection, square and accumulation
+        fused; no lambdas tensor)."""
+        jobs, fresh = [], []
         for layer in self.model.modules():
             if layer.__class__.__name__ in self.layer_types:
                 if layer.__class__.__name__ in ['Linear', 'Conv2d']:
@@ -822,15 +825,24 @@ class EFB(Curvature):
                         grads = torch.cat([grads, layer.bias.grad.unsqueeze(dim=1)], dim=1)
                     N.require_device(grads, "weight grad", layer)
                     V_A, V_G = self.eigvecs[layer]
-                    lambdas = (V_G.t() @ grads @ V_A) ** 2
                     if layer in self._state:
-                        self._state[layer] += lambdas
-                        self.diags[layer] += grads ** 2 * batch_size
+                        state, diag, accumulate = self._state[layer], self.diags[layer], True
                     else:
-                        self._state[layer] = lambdas
-                        self.diags[layer] = grads ** 2 * batch_size
+                        state = torch.empty_like(grads)
+                        diag = torch.empty_like(grads)
+                        accumulate = False
+                        fresh.append((layer, state, diag))
+                    jobs.append(N.efb_job(V_A, V_G, grads, state, diag, accumulate, batch_size))
                 elif layer.__class__.__name__ == 'MultiheadAttention':
                     raise NotImplementedError
+        if jobs:
+            N.efb_update(jobs, self._device_of(jobs))
+        for layer, state, diag in fresh:
+            self._state[layer] = state
+            self.diags[layer] = diag
+
+    def _device_of(self, jobs):
+        return next(iter(self.eigvecs.values()))[0].device
 
     def invert(self, add: Union[float, list, tuple] = 0., multiply: Union[float, list, tuple] = 1.):
         """curvatures.py:451-464: inv_state = (s * lambda + n)^{-1/2}, elementwise.  The
@@ -922,13 +934,15 @@ class INF(Curvature):
                     reg_inv_correction: Tensor) -> Tensor:
         """curvatures.py:548-580.  V_s = c * kron(U_A, U_G) diag(sigma) is never formed:
         (V_s^T V_s)[(p,q),(p',q')] = sigma sigma' sum_a U_A[a,p] U_A[a,p'] T[a,q,q'],
-        T[a] = U_G^T diag(c[a,:]^2) U_G."""
-        nA, la = frst_eigvecs.shape
-        nG, lg = scnd_eigvecs.shape
-        c2 = (reg_inv_correction.view(nA, nG) ** 2)
-        T = torch.einsum('ag,gq,gQ->aqQ', c2, scnd_eigvecs, scnd_eigvecs)
-        vtv = torch.einsum('ap,aP,aqQ->pqPQ', frst_eigvecs, frst_eigvecs, T).reshape(la * lg, la * lg)
-        vtv = reg_lambda[:, None] * vtv * reg_lambda[None, :]
+        T[a] = U_G^T diag(c[a,:]^2) U_G -- two device GEMMs (kfac_kron_gram) whose
+        operands are formed in the panel loaders."""
+        vtv = N.kron_gram(frst_eigvecs, scnd_eigvecs, reg_inv_correction, reg_lambda)
+        return INF._pre_sample_from_gram(vtv, reg_lambda)
+
+    @staticmethod
+    def _pre_sample_from_gram(vtv: Tensor, reg_lambda: Tensor) -> Tensor:
+        """curvatures.py:567-580 on the scaled Gram matrix (the reference's symmetrisation,
+        then its Cholesky / inverse sequence)."""
         vtv = (vtv + vtv.t()) / 2.
         eye = torch.eye(vtv.shape[0], device=vtv.device, dtype=vtv.dtype)
         A_c_inv = torch.linalg.cholesky(vtv).inverse()

@@ -234,6 +234,57 @@ KFAC_API size_t kfac_sample_workspace_bytes(const kfac_sample_job* jobs, int njo
 KFAC_API int kfac_sample(const kfac_sample_job* jobs, int njobs, int accumulate, void* workspace,
                 size_t workspace_bytes, kfac_stream_t stream);
 
+/* ------------------------------------------------ eigenbasis curvatures
+ * kfac_efb_update: EFB.update (models/curvatures.py:427-449) for up to 8 layers:
+ *   state = [state +] (VG^T grad VA) ** 2          (nG x nA, elementwise square)
+ *   diag  = [diag  +] (grad ** 2) * scale           (scale = batch size; diag may be NULL)
+ * grad is the layer's (nG x nA) weight gradient with the bias gradient as its last
+ * column; VA (nA x nA) and VG (nG x nG) the factors' eigenvectors (columns).  "+"
+ * when accumulate != 0, else the results are written.  Two launches; the projection
+ * VG^T grad lives in the workspace (nG x nA floats per layer).                  */
+typedef struct kfac_efb_job {
+  const float* VA;
+  int64_t ldA;
+  const float* VG;
+  int64_t ldG;
+  const float* grad;
+  int64_t ld_grad;
+  float* state;
+  int64_t ld_state;
+  float* diag;
+  int64_t ld_diag;
+  int32_t nA, nG;
+  int32_t accumulate;
+  float scale;
+} kfac_efb_job;
+
+KFAC_API size_t kfac_efb_workspace_bytes(const kfac_efb_job* jobs, int njobs);
+KFAC_API int kfac_efb_update(const kfac_efb_job* jobs, int njobs, void* workspace, size_t workspace_bytes,
+                             kfac_stream_t stream);
+
+/* kfac_kron_gram: INF.pre_sampler's V_s^T V_s (curvatures.py:548-580), V_s =
+ * c * kron(UA, UG) * sigma, without forming V_s ((nA*nG) x (la*lg)):
+ *   out[(p*lg+q)*ldo + p2*lg+q2] = sigma[p*lg+q] * sum_{a,g} c[a*nG+g]^2 UA[a][p] UA[a][p2]
+ *                                  UG[g][q] UG[g][q2] * sigma[p2*lg+q2]
+ * UA (nA x la, ldA), UG (nG x lg, ldG), c (nA*nG), sigma (la*lg).  Symmetric up
+ * to one rounding of the sigma scaling.  Workspace: nA x lg^2 floats per job; up
+ * to 8 jobs.                                                                    */
+typedef struct kfac_gram_job {
+  const float* UA;
+  int64_t ldA;
+  const float* UG;
+  int64_t ldG;
+  const float* c;
+  const float* sigma;
+  float* out;
+  int64_t ldo;
+  int32_t nA, nG, la, lg;
+} kfac_gram_job;
+
+KFAC_API size_t kfac_gram_workspace_bytes(const kfac_gram_job* jobs, int njobs);
+KFAC_API int kfac_kron_gram(const kfac_gram_job* jobs, int njobs, void* workspace, size_t workspace_bytes,
+                            kfac_stream_t stream);
+
 /* ------------------------------------------------- packed lower triangles
  * For the data-parallel collectives (no reference counterpart: the reference is
  * single-device).  Row i of a factor's lower triangle lives at

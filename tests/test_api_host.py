@@ -264,10 +264,13 @@ def test_variance_helpers():
 
 def test_inf_host_algebra_matches_literal_oracle():
     """INF's tensor restatements (curvatures.py:614-682: index arithmetic, the per-row
-    kron loop; :548-580 the pre-sample) against the literal loop/kron oracle.  These
-    are torch algebra on whatever device the tensors live; here CPU, no kernel call."""
+    kron loop; :548-580 the pre-sample after the Gram matrix) against the literal
+    loop/kron oracle.  These are torch algebra on whatever device the tensors live;
+    here CPU, no kernel call.  The Gram matrix itself is device-only."""
     import numpy as np
     import torch
+    import pytest
+    from bnn_kfac_amd import _native as N
     from bnn_kfac_amd.curvatures import INF
     from oracle import kfac_oracle as O
     rng = np.random.default_rng(3)
@@ -284,8 +287,13 @@ def test_inf_host_algebra_matches_literal_oracle():
         np.testing.assert_allclose(d, O.inf_diagonal_accumulator(wa, wb, wl), rtol=1e-12)
         sig = np.sqrt(200 * np.asarray(wl))
         c = 1.0 / np.sqrt(200 * rng.random(36) + 0.04)
-        P = INF.pre_sampler(a, b, torch.from_numpy(sig), torch.from_numpy(c)).numpy()
+        # the pre-sample's linear algebra after the Gram matrix (the Gram itself is
+        # kfac_kron_gram on the device: pre_sampler has no host path)
+        Vs = c[:, None] * np.kron(wa, wb) * sig[None, :]
+        P = INF._pre_sample_from_gram(torch.from_numpy(Vs.T @ Vs), torch.from_numpy(sig)).numpy()
         np.testing.assert_allclose(P, O.inf_pre_sampler(wa, wb, sig, c), rtol=1e-8, atol=1e-12)
+        with pytest.raises(N.NativeError):
+            INF.pre_sampler(a, b, torch.from_numpy(sig), torch.from_numpy(c))
 
 
 def test_sample_has_no_cpu_fallback():

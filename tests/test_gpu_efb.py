@@ -131,3 +131,44 @@ def test_efb_save_load_roundtrip(hip_device, tmp_path):
     for m in (net[0], net[3]):
         assert torch.equal(other.state[m], efb.state[m])
         assert torch.equal(other.inv_state[m], efb.inv_state[m])
+
+
+@pytest.mark.parametrize("nA,nG", [(785, 128), (129, 10), (70, 33)])
+def test_efb_update_kernel_vs_fp64(hip_device, nA, nG):
+    """kfac_efb_update directly: two accumulated batches, projection/square/diag
+    fused, against fp64 (rtol 1e-4 of max lambda: fp32 MFMA GEMMs; diag bit-exact:
+    (g * g) * B rounded as torch's grads ** 2 * batch_size then +=)."""
+    from bnn_kfac_amd import _native as N
+    rng = np.random.default_rng(nA + nG)
+    VA = np.linalg.qr(rng.standard_normal((nA, nA)))[0].astype(np.float32)
+    VG = np.linalg.qr(rng.standard_normal((nG, nG)))[0].astype(np.float32)
+    grads = [rng.standard_normal((nG, nA)).astype(np.float32) * 0.1 for _ in range(2)]
+    d = lambda x: torch.from_numpy(x).to(hip_device)
+    state = torch.full((nG, nA), np.nan, device=hip_device)
+    diag = torch.full((nG, nA), np.nan, device=hip_device)
+    for i, g in enumerate(grads):
+        N.efb_update([N.efb_job(d(VA), d(VG), d(g), state, diag, i > 0, 32)], hip_device)
+    want = sum((VG.T.astype(np.float64) @ g @ VA) ** 2 for g in grads)
+    got = state.cpu().numpy()
+    np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-4 * want.max())
+    gd = [torch.from_numpy(g) for g in grads]
+    want_d = (gd[0] ** 2 * 32 + gd[1] ** 2 * 32).numpy()
+    np.testing.assert_array_equal(diag.cpu().numpy(), want_d)
+
+
+@pytest.mark.parametrize("nA,nG,la,lg", [(50, 20, 7, 5), (300, 40, 33, 17), (785, 10, 9, 10)])
+def test_kron_gram_vs_explicit_kron(hip_device, nA, nG, la, lg):
+    """kfac_kron_gram (INF's V_s^T V_s without V_s) against the explicit kron in fp64:
+    rtol 1e-5 of the largest entry; symmetric to one rounding of the sigma scaling."""
+    from bnn_kfac_amd import _native as N
+    rng = np.random.default_rng(nA * lg + la)
+    UA = (rng.standard_normal((nA, la)) / np.sqrt(nA)).astype(np.float32)
+    UG = (rng.standard_normal((nG, lg)) / np.sqrt(nG)).astype(np.float32)
+    c = (rng.random(nA * nG) + 0.5).astype(np.float32)
+    sig = (rng.random(la * lg) + 0.5).astype(np.float32)
+    d = lambda x: torch.from_numpy(x).to(hip_device)
+    got = N.kron_gram(d(UA), d(UG), d(c), d(sig)).cpu().numpy()
+    Vs = c.astype(np.float64)[:, None] * np.kron(UA.astype(np.float64), UG.astype(np.float64))
+    want = sig[:, None] * (Vs.T @ Vs) * sig[None, :]
+    np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-5 * np.abs(want).max())
+    np.testing.assert_allclose(got, got.T, rtol=2.5e-7, atol=0)
