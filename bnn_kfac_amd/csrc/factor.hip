@@ -501,7 +501,10 @@ __device__ __forceinline__ void split3(float a, float b, uint32_t& h, uint32_t& 
 // (register ring).  Its stores put both columns' 8 k of a part in two 16-byte
 // chunks: the 8 lanes of a ds_write_b128 group hit 4 distinct bank groups twice
 // (2-way; the 2-column-apart mapping that avoided it needed twice the loads).
-constexpr int S3_DEPTH = 3;
+#ifndef KFAC_S3_DEPTH
+#define KFAC_S3_DEPTH 3  // (compile-time: the ring-depth A/B builds)
+#endif
+constexpr int S3_DEPTH = KFAC_S3_DEPTH;
 struct S3Prod {
   int vob[8];       // byte offset of row 8q + r of the pair (OOB: a fill pair)
   uint32_t hfill;   // the bias ones column's hi part (bf16 1.0 pair) on its lanes, else 0
