@@ -816,7 +816,10 @@ class EFB(Curvature):
         """curvatures.py:427-449: state += (V_G^T grad V_A)^2, diags += grad^2 * B --
         every layer in one kfac_efb_update call (projection, square and accumulation
         fused; no lambdas tensor)."""
-        jobs, fresh = [], []
+        # `keep`: the per-layer gradient matrices (torch.cat results) stay referenced
+        # until the launch is queued -- a freed one could be handed by the caching
+        # allocator to the next layer's tensors before the kernel reads it
+        jobs, fresh, keep = [], [], []
         for layer in self.model.modules():
             if layer.__class__.__name__ in self.layer_types:
                 if layer.__class__.__name__ in ['Linear', 'Conv2d']:
@@ -833,10 +836,12 @@ class EFB(Curvature):
                         accumulate = False
                         fresh.append((layer, state, diag))
                     jobs.append(N.efb_job(V_A, V_G, grads, state, diag, accumulate, batch_size))
+                    keep.append(grads)
                 elif layer.__class__.__name__ == 'MultiheadAttention':
                     raise NotImplementedError
         if jobs:
             N.efb_update(jobs, self._device_of(jobs))
+        del keep
         for layer, state, diag in fresh:
             self._state[layer] = state
             self.diags[layer] = diag
