@@ -285,7 +285,9 @@ def spawn_ranks(n, argv, cmd=None, check_devices=True, poll_s=0.2):
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    # 50 steps: the timed region ends with the last inversion's drain (~0.5 ms on the
+    # MLP, not overlapped by a next pass), 8 % of a 10-step region, <2 % of 50
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="mlp", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="per-rank batch (default: the config's)")
