@@ -1128,30 +1128,36 @@ __global__ __launch_bounds__(NTHREADS) void kfac_factor_channel_small(FactorArgs
   float acc[NT];
 #pragma unroll
   for (int e = 0; e < NT; ++e) acc[e] = 0.f;
-  int64_t img = tid / L4, r4 = tid - img * L4;
-  const int64_t dimg = NTHREADS / L4, dr = NTHREADS - dimg * L4;
-  for (int64_t q = tid; q < per; q += NTHREADS) {
+  // two (image, run) pairs per trip, their 2 x n float4 loads issued together
+  auto src_of = [&](int64_t q) {
+    const int64_t img = q / L4, r4 = q - img * L4;
     // image b0 + img of the job: batch seg of the queued batches, image bi in it
     const uint32_t ab = (uint32_t)(b0 + img), seg = ab / (uint32_t)cg.bseg;
-    const float* src = seg_base(J, args.segs, (int)seg) + (int64_t)(ab - seg * cg.bseg) * op.sB + 4 * r4;
-    floatx4 x[NMAX];
+    return seg_base(J, args.segs, (int)seg) + (int64_t)(ab - seg * cg.bseg) * op.sB + 4 * r4;
+  };
+  for (int64_t q = tid; q < per; q += 2 * NTHREADS) {
+    const bool two = q + NTHREADS < per;
+    const float* s0 = src_of(q);
+    const float* s1 = two ? src_of(q + NTHREADS) : s0;
+    floatx4 x[2][NMAX];
 #pragma unroll
     for (int c = 0; c < NMAX; ++c) {
-      if (c < n) x[c] = *reinterpret_cast<const floatx4*>(src + c * op.L);
-      else x[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+      const bool in = c < n;  // (channels past n: zero rows of the triangle)
+      x[0][c] = in ? *reinterpret_cast<const floatx4*>(s0 + c * op.L) : floatx4{0.f, 0.f, 0.f, 0.f};
+      x[1][c] = in ? *reinterpret_cast<const floatx4*>(s1 + c * op.L) : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (!two) {
+#pragma unroll
+      for (int c = 0; c < NMAX; ++c) x[1][c] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int i = 0, e = 0; i < NMAX; ++i)
+      for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int j = 0; j <= i; ++j, ++e) acc[e] = fmaf(x[i][u], x[j][u], acc[e]);
-    img += dimg;
-    r4 += dr;
-    if (r4 >= L4) {
-      r4 -= L4;
-      ++img;
-    }
+        for (int i = 0, e = 0; i < NMAX; ++i)
+#pragma unroll
+          for (int j = 0; j <= i; ++j, ++e) acc[e] = fmaf(x[h][i][u], x[h][j][u], acc[e]);
   }
 #pragma unroll
   for (int e = 0; e < NT; ++e) {
@@ -1264,7 +1270,14 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
 template <int LAYOUT>
 static void launch_conv(const FactorArgs& args, const ConvGeom& g, int tasks, hipStream_t stream) {
   if (LAYOUT == KFAC_CHANNEL && g.n <= 8 && !conv_small_off()) {
-    hipLaunchKernelGGL(kfac_factor_channel_small<8>, dim3(tasks), dim3(NTHREADS), 0, stream, args, g);
+    // the exact channel count (LeNet-5 conv1: 6) sizes the register triangle and its
+    // reduction; other counts take the next instance up (their extra rows are zero)
+    if (g.n == 6)
+      hipLaunchKernelGGL(kfac_factor_channel_small<6>, dim3(tasks), dim3(NTHREADS), 0, stream, args, g);
+    else if (g.n <= 4)
+      hipLaunchKernelGGL(kfac_factor_channel_small<4>, dim3(tasks), dim3(NTHREADS), 0, stream, args, g);
+    else
+      hipLaunchKernelGGL(kfac_factor_channel_small<8>, dim3(tasks), dim3(NTHREADS), 0, stream, args, g);
     return;
   }
   const size_t shmem = (size_t)g.lds * sizeof(float);
