@@ -38,6 +38,7 @@ struct FactorJobDev {
   int tile_begin;    // first global tile of this job (reduce launch)
   int accum;         // deferred reduction: `slab` is the caller's accumulator
   float sbeta;       // accumulator update: slab = sbeta*slab + alpha*partial
+  char* split3;      // pre-split bf16x3 panel images of the job (kfac_factor_syrk3), else null
 };
 
 struct FactorArgs {
@@ -229,6 +230,10 @@ __device__ __forceinline__ void vm_wait(int n) {
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
@@ -442,31 +447,27 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
 // (v_mfma_f32_32x32x2_f32), so six of them are 2.67x the fp32 MFMA rate: the
 // roofline of this kernel is 2.5 PF / 6 = 417 TF/s of fp32-equivalent work.
 //
-// Work unit: one 128 x 128 macro tile (= 2 x 2 of the 64-tiles whose partial slabs
-// the reduce sums) of one factor over one K-chunk; one workgroup per CU (96 KB of
-// LDS), 768 threads in two roles, one consumer and two producers per SIMD:
-//   consumers (waves 0-3): wave w computes the 64 x 64 quadrant (w >> 1, w & 1) =
-//     2 x 2 blocks of 32 x 32 -- fragment reads and MFMAs only;
-//   producers (waves 4-11; 4-7 the A panel, 8-11 the B panel): load the next
-//     stage's rows, split them into the three bf16 parts and store them -- global
-//     loads, VALU and LDS stores only,
-// so each SIMD's MFMA pipe is fed by one wave while two others do the conversion
-// work beside it (one producer wave per SIMD measured as the critical path: the
-// kernel took 88 % as long with the MFMAs removed); one barrier per stage hands the
-// stage over (double-buffered).  A stage = 32 rows of K; a producer thread takes 8
-// rows of 2 columns of its panel.  LDS image per stage: two substep regions
-// (k 0-15, 16-31), each [part][column][2 chunks of 8 k] (32 B per column, k
+// Two launches per grouped update:
+//   kfac_split3        streams each 32-row stage of each 128-column panel of the
+//                      operand ONCE into its three bf16 parts, laid out byte for byte
+//                      as the SYRK's LDS image of that panel (HBM-bound, 4 B read +
+//                      6 B written per element);
+//   kfac_factor_syrk3  one 128 x 128 macro tile (= 2 x 2 of the 64-tiles whose
+//                      partial slabs the reduce sums) of one factor over one K-chunk
+//                      per workgroup: wave w computes the 64 x 64 quadrant (w >> 1,
+//                      w & 1) as 2 x 2 blocks of 32 x 32; the panel images arrive by
+//                      LDS-DMA (global_load_lds_dwordx4) into a ring of 16-row
+//                      k-substeps -- no staging registers, no VALU in the loop.
+// LDS image of a substep: [part][column][2 chunks of 8 k] (32 B per column, k
 // contiguous), read straight into MFMA operands (lane = column, 8 k per
-// ds_read_b128).  The chunk of a column is XOR-swizzled by bit 3 of the column and
-// the second region is offset by 64 B mod 128: fragment reads and the stores are
-// both conflict-free, and every fragment read is a per-lane base plus an immediate.
+// ds_read_b128); the chunk of a column is XOR-swizzled by bit 3 of the column, so the
+// fragment reads are conflict-free and each is a per-lane base plus an immediate.
+// (A first version split in 8 producer waves beside 4 consumer waves per workgroup:
+// producer-bound at 0.25 of the roofline)
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int MT = 128;                          // macro tile edge
-constexpr int S3_THREADS = 768;
-constexpr int S3_PART = 2 * MT * 32;             // bytes of one part of one substep region
-constexpr int S3_REG = 3 * S3_PART + 64;         // substep region (+64: store banks)
-constexpr int S3_STAGE = 2 * S3_REG;
-constexpr int S3_LDS = 2 * S3_STAGE;             // two stages: 98,560 bytes
+constexpr int S3_PART = 2 * MT * 32;             // bytes of one part of a substep slot (A and B)
+constexpr int S3_REG = 3 * S3_PART + 64;         // one substep slot (+64: bank offset)
 
 // byte offset of half-chunk hh (k 8hh .. 8hh+7 of a substep) of column c in a part
 __device__ __forceinline__ int s3_half(int c, int hh) { return c * 32 + ((hh ^ ((c >> 3) & 1)) << 4); }
@@ -496,130 +497,13 @@ __device__ __forceinline__ void split3(float a, float b, uint32_t& h, uint32_t& 
   l = bf16_pair(sa, sb);
 }
 
-// A producer thread's share of a stage: rows 8q .. 8q+7 of the column pair 2g, 2g+1
-// of its panel (one 8-byte load per row).  S3_DEPTH stages of loads are in flight
-// (register ring).  Its stores put both columns' 8 k of a part in two 16-byte
-// chunks: the 8 lanes of a ds_write_b128 group hit 4 distinct bank groups twice
-// (2-way; the 2-column-apart mapping that avoided it needed twice the loads).
-#ifndef KFAC_S3_DEPTH
-#define KFAC_S3_DEPTH 3  // (compile-time: the ring-depth A/B builds)
-#endif
-constexpr int S3_DEPTH = KFAC_S3_DEPTH;
-struct S3Prod {
-  int vob[8];       // byte offset of row 8q + r of the pair (OOB: a fill pair)
-  uint32_t hfill;   // the bias ones column's hi part (bf16 1.0 pair) on its lanes, else 0
-  int off0, off1;   // LDS byte offsets of the two columns' chunks in a stage
-  int q;
-};
-typedef float S3Rows[2][8];  // [column][row] of one stage
-
-// The producer's stage cursor: the stage's first row as a uniform base pointer,
-// advanced by 32 rows per stage (a new batch base at a batch boundary).
-struct S3Cur {
-  const float* bp;
-  int64_t k;
-  int seg;
-  __device__ __forceinline__ void init(const FactorJobDev& J, const float* const* segs, int64_t s, int ld) {
-    seg = (int)(s / J.sps);
-    k = (s - (int64_t)seg * J.sps) * BK;
-    bp = seg_base(J, segs, seg) + k * ld;
-  }
-  __device__ __forceinline__ void next(const FactorJobDev& J, const float* const* segs, int ld) {
-    k += BK;
-    bp += (int64_t)BK * ld;
-    if (k >= J.x.rows) {
-      k = 0;
-      ++seg;
-      bp = seg_base(J, segs, seg);
-    }
-  }
-};
-
-// loads of the stage at `cur` into v (returns its real rows): raw buffer loads of
-// the stage's rows (base and size uniform, from SGPRs) at per-thread byte offsets;
-// rows past the batch and fill columns fall outside the buffer and read 0 (the ones
-// column gets its 1 at the commit)
-__device__ __forceinline__ int s3_load(const S3Prod& P, S3Rows& v, const FactorJobDev& J,
-                                       const float* const* segs, S3Cur& cur, int ld) {
-  const uint64_t bpu = reinterpret_cast<uint64_t>(cur.bp);
-  // (uniform by construction; readfirstlane tells the compiler, else it wraps every
-  // buffer load in a waterfall loop.  readfirstlane returns int: zero-extend)
-  void* bp = reinterpret_cast<void*>(
-      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(bpu >> 32)) << 32) |
-      (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)bpu));
-  const int64_t left = J.x.rows - cur.k;
-  const int nrow = __builtin_amdgcn_readfirstlane(left < BK ? (int)left : BK);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      bp, (short)0, __builtin_amdgcn_readfirstlane(nrow * ld * 4), 0x00020000);
-  typedef float float2v __attribute__((ext_vector_type(2)));
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const float2v x = __builtin_bit_cast(float2v, __builtin_amdgcn_raw_buffer_load_b64(rs, P.vob[r], 0, 0));
-    v[0][r] = x[0];
-    v[1][r] = x[1];
-  }
-  cur.next(J, segs, ld);
-  return nrow;
-}
-
-// v -> hi / mid / lo parts -> the thread's chunks of a stage (`nrow` real rows).  The
-// 8 pair-splits run step by step side by side (independent chains between the
-// conversions, which need wait states before their results are read); the ones
-// column's 1.0 is OR-ed into its hi part (its loads read 0).
-__device__ __forceinline__ void s3_commit(const S3Prod& P, S3Rows& v, int nrow, char* stage) {
-  uint32_t h[2][4], m[2][4], l[2][4];
-  float ra[2][4], rb[2][4];
-#pragma unroll
-  for (int c = 0; c < 2; ++c)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) h[c][i] = bf16_pair(v[c][2 * i], v[c][2 * i + 1]);
-#pragma unroll
-  for (int c = 0; c < 2; ++c)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      ra[c][i] = sub_f32(v[c][2 * i], __uint_as_float(h[c][i] << 16));
-      rb[c][i] = sub_f32(v[c][2 * i + 1], __uint_as_float(h[c][i] & 0xffff0000u));
-    }
-#pragma unroll
-  for (int c = 0; c < 2; ++c)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) m[c][i] = bf16_pair(ra[c][i], rb[c][i]);
-#pragma unroll
-  for (int c = 0; c < 2; ++c)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      ra[c][i] = sub_f32(ra[c][i], __uint_as_float(m[c][i] << 16));
-      rb[c][i] = sub_f32(rb[c][i], __uint_as_float(m[c][i] & 0xffff0000u));
-    }
-#pragma unroll
-  for (int c = 0; c < 2; ++c)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) l[c][i] = bf16_pair(ra[c][i], rb[c][i]);
-  if (nrow == BK) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) h[0][i] |= P.hfill;
-  } else {  // a partial stage: the ones column only on its real rows
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = 8 * P.q + 2 * i;
-      h[0][i] |= P.hfill & ((r < nrow ? 0x0000ffffu : 0u) | (r + 1 < nrow ? 0xffff0000u : 0u));
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    char* d = stage + (c ? P.off1 : P.off0);
-    *reinterpret_cast<uint4*>(d) = make_uint4(h[c][0], h[c][1], h[c][2], h[c][3]);
-    *reinterpret_cast<uint4*>(d + S3_PART) = make_uint4(m[c][0], m[c][1], m[c][2], m[c][3]);
-    *reinterpret_cast<uint4*>(d + 2 * S3_PART) = make_uint4(l[c][0], l[c][1], l[c][2], l[c][3]);
-  }
-}
-
-// A consumer wave's MFMAs on one stage: blocks (bi, bj) of its 64 x 64 quadrant with
-// act[bi][bj], six products per block and k-16 substep.  oa / ob: this lane's A / B
-// fragment offsets (substep 0, part 0, block 0); everything else is an immediate.
-__device__ __forceinline__ void s3_consume(const char* stage, int oa, int ob, const bool (&act)[2][2],
-                                           floatx16 (&acc)[2][2]) {
-  auto frag = [&](int off) { return *reinterpret_cast<const bf16x8*>(stage + off); };
+// A wave's MFMAs on one 16-row k-substep (the slot at `reg`): blocks (bi, bj) of its
+// 64 x 64 quadrant with act[bi][bj], six products per block.  oa / ob: this lane's A / B
+// fragment offsets (part 0, block 0); everything else is an immediate.  The 12
+// fragments go out first, then the MFMAs.
+__device__ __forceinline__ void s3_consume_sub(const char* reg, int oa, int ob, const bool (&act)[2][2],
+                                               floatx16 (&acc)[2][2]) {
+  auto frag = [&](int off) { return *reinterpret_cast<const bf16x8*>(reg + off); };
   auto six = [&](int bi, int bj, const bf16x8* A, const bf16x8* B) {
     if (!act[bi][bj]) return;
     acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], acc[bi][bj], 0, 0, 0);
@@ -629,9 +513,6 @@ __device__ __forceinline__ void s3_consume(const char* stage, int oa, int ob, co
     acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], acc[bi][bj], 0, 0, 0);
     acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], acc[bi][bj], 0, 0, 0);
   };
-  // fragments are read in the order they die, so at most 15 are live (60 VGPRs: with
-  // all 24 of a stage live the 768-thread workgroup filled the SIMDs' register files
-  // and the overlapped inversion's workgroups could not start beside it)
   bf16x8 a0[3], a1[3], b0[3], b1[3];
 #pragma unroll
   for (int p = 0; p < 3; ++p) {
@@ -639,18 +520,6 @@ __device__ __forceinline__ void s3_consume(const char* stage, int oa, int ob, co
     b0[p] = frag(ob + p * S3_PART);
     b1[p] = frag(ob + p * S3_PART + 32 * 32);
     a1[p] = frag(oa + p * S3_PART + 32 * 32);
-  }
-  six(0, 0, a0, b0);
-  six(0, 1, a0, b1);
-#pragma unroll
-  for (int p = 0; p < 3; ++p) a0[p] = frag(oa + S3_REG + p * S3_PART);
-  six(1, 0, a1, b0);
-  six(1, 1, a1, b1);
-#pragma unroll
-  for (int p = 0; p < 3; ++p) {
-    b0[p] = frag(ob + S3_REG + p * S3_PART);
-    b1[p] = frag(ob + S3_REG + p * S3_PART + 32 * 32);
-    a1[p] = frag(oa + S3_REG + p * S3_PART + 32 * 32);
   }
   six(0, 0, a0, b0);
   six(0, 1, a0, b1);
@@ -688,8 +557,62 @@ __device__ __forceinline__ void s3_decode(int unit, int T3, int& I, int& J) {
   }
 }
 
-__device__ __forceinline__ void s3_task(const FactorJobDev& J, const float* const* segs, int local,
-                                        char* lds) {
+// ------------------------------------------- bf16x3 SYRK: split pass and SYRK
+// The ring: NSLOT single-substep slots (24,640 B each) per workgroup, NSLOT - 1 in
+// flight, one barrier per substep; S3D_WGS workgroups per CU (256 threads, one wave
+// per SIMD each) interleave their barriers and DMA waits.  2 slots x 3 workgroups
+// measured best on the wide C5 line.
+constexpr int S3_PANEL = 2 * 3 * MT * 32;  // bytes of one panel's split stage (24 KB)
+#ifndef KFAC_S3D_NSLOT
+#define KFAC_S3D_NSLOT 2  // (compile-time: the ring-depth A/B builds)
+#endif
+#ifndef KFAC_S3D_WGS
+#define KFAC_S3D_WGS 3  // resident workgroups per CU the planner counts on
+#endif
+constexpr int S3D_NSLOT = KFAC_S3D_NSLOT;
+constexpr int S3D_WGS = KFAC_S3D_WGS;
+constexpr int S3D_LDS = S3D_NSLOT * S3_REG;
+
+// one (stage, panel) of one job per workgroup: thread (c = t & 127, h = t >> 7) takes
+// column c's rows 8h .. 8h+7 (region 0) and 16 + 8h .. (region 1)
+__global__ __launch_bounds__(NTHREADS) void kfac_split3(FactorArgs args) {
+  const int task = blockIdx.x;
+  int j = 0;
+  while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
+  const FactorJobDev& J = args.job[j];
+  const int T3 = (J.n + MT - 1) / MT;
+  const int local = task - J.task_begin;
+  const int64_t st = local / T3;
+  const int panel = local - (int)st * T3;
+  const int seg = (int)(st / J.sps);
+  const int64_t k0 = (st - (int64_t)seg * J.sps) * BK;
+  const float* base = seg_base(J, args.segs, seg);
+  const int ld = (int)J.x.ld;
+  const int nrow = (int)min((int64_t)BK, J.x.rows - k0);
+  const int c = threadIdx.x & 127, h = threadIdx.x >> 7;
+  const int col = panel * MT + c;
+  const bool real = col < J.x.cols, ones = col == J.x.ones;
+  char* out = J.split3 + ((size_t)st * T3 + panel) * S3_PANEL;
+#pragma unroll
+  for (int reg = 0; reg < 2; ++reg) {
+    const int r0 = 16 * reg + 8 * h;
+    float v[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int row = r0 + r;
+      v[r] = row < nrow ? (real ? base[(k0 + row) * ld + col] : (ones ? 1.f : 0.f)) : 0.f;
+    }
+    uint32_t p0[4], p1[4], p2[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) split3(v[2 * i], v[2 * i + 1], p0[i], p1[i], p2[i]);
+    char* d = out + reg * 3 * MT * 32 + s3_half(c, h);
+    *reinterpret_cast<uint4*>(d) = make_uint4(p0[0], p0[1], p0[2], p0[3]);
+    *reinterpret_cast<uint4*>(d + MT * 32) = make_uint4(p1[0], p1[1], p1[2], p1[3]);
+    *reinterpret_cast<uint4*>(d + 2 * MT * 32) = make_uint4(p2[0], p2[1], p2[2], p2[3]);
+  }
+}
+
+__device__ __forceinline__ void s3d_task(const FactorJobDev& J, int local, char* lds) {
   const int T3 = (J.n + MT - 1) / MT, units = T3 * (T3 + 1) / 2;
   const int split = local / units, unit = local - split * units;
   int I, Jc;
@@ -700,114 +623,83 @@ __device__ __forceinline__ void s3_task(const FactorJobDev& J, const float* cons
   const int ns = (int)(s1 - s0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (wave < 4) {
-    // ---------------------------------------------------------------- consumer
-    // issue priority over the two producer waves on the SIMD: an MFMA that is ready
-    // goes first, the producers' VALU work fills the MFMA's shadow
-    __builtin_amdgcn_s_setprio(2);
-    const int wr = wave >> 1, wc = wave & 1;
-    bool act[2][2];
+  const int wr = wave >> 1, wc = wave & 1;
+  bool act[2][2];
 #pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
+  for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-      for (int bj = 0; bj < 2; ++bj) {
-        const int r0 = I * MT + wr * 64 + bi * 32, c0 = Jc * MT + wc * 64 + bj * 32;
-        act[bi][bj] = r0 < J.n && c0 < J.n && r0 >= c0;
-      }
-    floatx16 acc[2][2];
-#pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-      for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) acc[bi][bj][v] = 0.f;
-    const int cl = lane & 31, lo = s3_half(cl, lane >> 5);
-    const int oa = wr * 64 * 32 + lo;
-    const int ob = ((same ? 0 : MT) + wc * 64) * 32 + lo;
-    const bool any = act[0][0] || act[0][1] || act[1][0] || act[1][1];
-    if (ns > 0) {
-      __syncthreads();  // stage 0 stored
-      for (int st = 0; st < ns; ++st) {
-        if (any) s3_consume(lds + (st & 1) * S3_STAGE, oa, ob, act, acc);
-        __syncthreads();  // stage st read; stage st+1 stored
-      }
+    for (int bj = 0; bj < 2; ++bj) {
+      const int r0 = I * MT + wr * 64 + bi * 32, c0 = Jc * MT + wc * 64 + bj * 32;
+      act[bi][bj] = r0 < J.n && c0 < J.n && r0 >= c0;
     }
-    // partials -> the 64-tile slabs: block (bi, bj) = quadrant (bi, bj) of 64-tile
-    // (2I + wr, 2Jc + wc)
-    const int ti = 2 * I + wr, tj = 2 * Jc + wc;
-    float* o = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.splits + split) * TILE * TILE;
+  const bool any = act[0][0] || act[0][1] || act[1][0] || act[1][1];
+  floatx16 acc[2][2];
 #pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
+  for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-      for (int bj = 0; bj < 2; ++bj)
-        if (act[bi][bj])
-          put_partial(J, acc[bi][bj],
-                      [&](int v) { return &o[(bi * 32 + acc_row(v, lane)) * TILE + bj * 32 + (lane & 31)]; });
-    return;
-  }
-  // ---------------------------------------------------------------- producer
-  if (ns <= 0) return;
-  // thread p of panel pn -> row chunk q = p & 3 and the column pair 2g, 2g + 1 (g = p >> 2).
-  // A diagonal tile has one panel: the B-panel waves only meet the barriers.
-  const int pn = (tid - 256) >> 8, p = tid & 255, q = p & 3, g = p >> 2;
-  const bool works = pn == 0 || !same;  // wave-uniform
-  const int ld = __builtin_amdgcn_readfirstlane((int)J.x.ld);  // (< 2^24: a stage's offsets fit 32 bits)
-  S3Prod P;
-  P.q = q;
-  P.off0 = (q >> 1) * S3_REG + s3_half(pn * MT + 2 * g, q & 1);
-  P.off1 = (q >> 1) * S3_REG + s3_half(pn * MT + 2 * g + 1, q & 1);
-  {
-    const int col = (pn ? Jc : I) * MT + 2 * g;
-    const bool real = col < J.x.cols;  // cols % 4 == 0: a pair is all real or all fill
-    P.hfill = (col == J.x.ones) ? 0x3f803f80u : 0u;  // bf16 (1.0, 1.0)
+    for (int bj = 0; bj < 2; ++bj)
 #pragma unroll
-    for (int r = 0; r < 8; ++r) P.vob[r] = real ? ((8 * q + r) * ld + col) * 4 : 0x7fffff00;
-  }
-  if (!works) {
-    for (int st = 0; st <= ns; ++st) __syncthreads();
-    return;
-  }
-  S3Cur cur;
-  cur.init(J, segs, s0, ld);
-  S3Rows v[S3_DEPTH];
-  int nr[S3_DEPTH];  // real rows of the stage in each ring slot
-  // stage i lives in ring slot i % S3_DEPTH; the loop is unrolled by the ring depth
-  // so every slot is a fixed register set
+      for (int v = 0; v < 16; ++v) acc[bi][bj][v] = 0.f;
+  const int cl = lane & 31, lo = s3_half(cl, lane >> 5);
+  const int oa = wr * 64 * 32 + lo;
+  const int ob = ((same ? 0 : MT) + wc * 64) * 32 + lo;
+  // DMA of one substep h (region h & 1 of stage s0 + h / 2): per panel 3 parts of
+  // 4 KB = 12 wave instructions of 1 KB; wave w takes instructions w, w + 4, w + 8
+  const char* pa = J.split3 + (size_t)I * S3_PANEL;
+  const char* pb = J.split3 + (size_t)Jc * S3_PANEL;
+  const size_t sstride = (size_t)T3 * S3_PANEL;
+  auto issue = [&](int hs) {
+    char* slot = lds + (hs % S3D_NSLOT) * S3_REG;
+    const size_t so = (size_t)(s0 + (hs >> 1)) * sstride + (size_t)(hs & 1) * 3 * MT * 32;
 #pragma unroll
-  for (int i = 0; i < S3_DEPTH; ++i)
-    if (i < ns) nr[i] = s3_load(P, v[i], J, segs, cur, ld);
-  s3_commit(P, v[0], nr[0], lds);
-  if (S3_DEPTH < ns) nr[0] = s3_load(P, v[0], J, segs, cur, ld);
-  __syncthreads();  // stage 0 stored
-  for (int st0 = 0; st0 < ns; st0 += S3_DEPTH) {
+    for (int q = 0; q < 3; ++q) {
+      const int i = wave + 4 * q;         // 0 .. 11
+      const int part = i >> 2, kb = i & 3;  // part, its 1 KB piece
+      const int go = part * (MT * 32) + kb * 1024;
+      const int lo_ = part * S3_PART + kb * 1024;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(pa + so + go + lane * 16),
+                                       slot + lo_, 16, 0, 0);
+      if (!same)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(pb + so + go + lane * 16),
+                                         slot + lo_ + MT * 32, 16, 0, 0);
+    }
+  };
+  const int per = same ? 3 : 6;  // DMA instructions per wave per substep
+  const int nh = 2 * ns;          // substeps of the task
+  if (nh > 0) {
 #pragma unroll
-    for (int u = 0; u < S3_DEPTH; ++u) {
-      const int st = st0 + u;  // consumers compute stage st; store stage st+1
-      if (st >= ns) break;
-      if (st + 1 < ns) {
-        const int sl = (u + 1) % S3_DEPTH;  // (a constant once unrolled)
-        s3_commit(P, v[sl], nr[sl], lds + ((st + 1) & 1) * S3_STAGE);
-        if (st + 1 + S3_DEPTH < ns) nr[sl] = s3_load(P, v[sl], J, segs, cur, ld);
-      }
-      __syncthreads();
+    for (int p0 = 0; p0 < S3D_NSLOT - 1; ++p0)
+      if (p0 < nh) issue(p0);
+    for (int hs = 0; hs < nh; ++hs) {
+      const int issued = min(nh - 1, hs + S3D_NSLOT - 2);  // last substep already issued
+      vm_wait(per * (issued - hs));
+      stage_barrier();  // substep hs landed for every wave; the slot of hs - 1 is free
+      if (hs + S3D_NSLOT - 1 < nh) issue(hs + S3D_NSLOT - 1);
+      if (any) s3_consume_sub(lds + (hs % S3D_NSLOT) * S3_REG, oa, ob, act, acc);
     }
   }
+  const int ti = 2 * I + wr, tj = 2 * Jc + wc;
+  float* o = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.splits + split) * TILE * TILE;
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+      if (act[bi][bj])
+        put_partial(J, acc[bi][bj],
+                    [&](int v) { return &o[(bi * 32 + acc_row(v, lane)) * TILE + bj * 32 + (lane & 31)]; });
 }
 
-__global__ __launch_bounds__(S3_THREADS, 1) void kfac_factor_syrk3(FactorArgs args) {
+__global__ __launch_bounds__(NTHREADS, S3D_WGS) void kfac_factor_syrk3(FactorArgs args) {
   extern __shared__ __attribute__((aligned(16))) char s3lds[];
   const int task = xcd_task(blockIdx.x, gridDim.x);
   int j = 0;
   while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
   const FactorJobDev& J = args.job[j];
   const int local = task - J.task_begin;
-  if (J.n <= 32) {
-    if (threadIdx.x < NTHREADS)  // the 4-wave narrow path (its barriers count 4 waves:
-      // the other 4 leave first, so they never meet a barrier)
-      factor_task_narrow_direct(J, args.segs, local, reinterpret_cast<float*>(s3lds));
-  } else {
-    s3_task(J, args.segs, local, s3lds);
-  }
+  if (J.n <= 32)
+    factor_task_narrow_direct(J, args.segs, local, reinterpret_cast<float*>(s3lds));
+  else
+    s3d_task(J, local, s3lds);
 }
 
 // ------------------------------------------------------------ conv operands
@@ -1402,15 +1294,23 @@ static bool job_glds(const kfac_factor_job& jb) {
 // bf16x3 SYRK (kfac_factor_syrk3) for a row-major launch group: every job either
 // LDS-eligible (16-byte rows, n > 32) or narrow (n <= 32, direct loads).
 // Default: a group whose largest factor has n >= 2048 (measured A/B, same box: wide
-// MLP 4097^2 factors 1.065e6 vs 9.37e5 img/s; the MNIST MLP's n <= 785 8.95e7 vs
-// 9.10e7 -- there the 28 macro tiles of a 785 factor leave the chip a quarter full
-// and the fp32 kernel's four workgroups per CU win).  KFAC_SYRK3=1 / 0 forces it.
+// MLP 4097^2 factors 1.17e6 vs 9.4e5 img/s; the MNIST MLP's n <= 785 8.1e7 vs 1.0e8
+// -- there the split pass's padded 6-byte images (785 -> 896, 129 -> 256 columns)
+// cost as much as the fp32 kernel's whole launch).  KFAC_SYRK3=1 / 0 forces it.
 static int syrk3_mode() {
   static const int m = [] {
     const char* v = getenv("KFAC_SYRK3");
     return v && v[0] == '1' ? 1 : v && v[0] == '0' ? 0 : -1;
   }();
   return m;
+}
+
+// bytes of a job's pre-split panel images (kfac_factor_syrk3; narrow jobs: none)
+static size_t split3_bytes(const kfac_factor_job& j) {
+  const int n = factor_n(j);
+  if (n <= 32) return 0;
+  const int64_t t3 = cdiv(n, MT);
+  return align_up((size_t)(job_sps(j) * job_nseg(j)) * (size_t)t3 * S3_PANEL, 256);
 }
 
 static bool syrk3_group(const kfac_factor_job* jobs, int njobs) {
@@ -1429,8 +1329,9 @@ static bool syrk3_group(const kfac_factor_job* jobs, int njobs) {
 static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
                       int64_t slots = 0) {
   const bool s3 = syrk3_group(jobs, njobs);
-  // resident workgroups per CU: 4 (32 KB of LDS each); the bf16x3 kernel: 1 (96 KB)
-  if (slots <= 0) slots = (s3 ? 1 : 4) * 256;
+  // resident workgroups per CU: 4 (32 KB of LDS each); the bf16x3 kernel: S3D_WGS
+  // (49 KB each)
+  if (slots <= 0) slots = (s3 ? S3D_WGS : 4) * 256;
   constexpr int64_t MIN_CHUNK = 8, OVERHEAD = 4;  // stages; ~per-task fixed cost in stages
   int64_t max_steps = 1;
   for (int i = 0; i < njobs; ++i) max_steps = std::max(max_steps, job_stages(jobs[i]));
@@ -1553,8 +1454,8 @@ static void launch_reduce(FactorArgs& r, int tiles, hipStream_t stream) {
 // workgroups) and the reduce of the jobs without an accumulator (`red`, `rtiles`
 // tiles).  Returns KFAC_EWORKSPACE when the slabs do not fit.
 struct GroupLaunch {
-  FactorArgs args, red;
-  int tasks, rtiles;
+  FactorArgs args, red, split;
+  int tasks, rtiles, split_tasks;
 };
 
 static int prepare_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t ws_bytes,
@@ -1602,6 +1503,23 @@ static int prepare_group(const kfac_factor_job* jobs, int njobs, char* ws, size_
   }
   g.tasks = tasks;
   g.rtiles = rtiles;
+  g.split_tasks = 0;
+  if (syrk3_group(jobs, njobs)) {
+    // the pre-split images after the slabs; the split launch's own task ranges
+    g.split = args;
+    int st = 0;
+    for (int i = 0; i < njobs; ++i) {
+      const size_t b = split3_bytes(jobs[i]);
+      args.job[i].split3 = b ? ws + off : nullptr;
+      off += b;
+      FactorJobDev& e = g.split.job[i];
+      e.split3 = args.job[i].split3;
+      e.task_begin = st;
+      if (b) st += (int)(job_stages(jobs[i]) * cdiv(factor_n(jobs[i]), MT));
+      g.split.task_end[i] = st;
+    }
+    g.split_tasks = st;
+  }
   return off > ws_bytes ? KFAC_EWORKSPACE : KFAC_OK;
 }
 
@@ -1641,9 +1559,13 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
           if (s3) {
             static const bool attr = hipFuncSetAttribute(
                 reinterpret_cast<const void*>(&kfac_factor_syrk3),
-                hipFuncAttributeMaxDynamicSharedMemorySize, S3_LDS) == hipSuccess;
+                hipFuncAttributeMaxDynamicSharedMemorySize, S3D_LDS) == hipSuccess;
             if (!attr) return KFAC_ELAUNCH;
-            hipLaunchKernelGGL(kfac_factor_syrk3, dim3(tasks), dim3(S3_THREADS), S3_LDS, stream, args);
+            if (g.split_tasks > 0) {
+              hipLaunchKernelGGL(kfac_split3, dim3(g.split_tasks), dim3(NTHREADS), 0, stream, g.split);
+              KFAC_CHECK_LAUNCH();
+            }
+            hipLaunchKernelGGL(kfac_factor_syrk3, dim3(tasks), dim3(NTHREADS), S3D_LDS, stream, args);
           } else if (all_glds)
             hipLaunchKernelGGL(kfac_factor_tiles_glds, dim3(tasks), dim3(NTHREADS), 0, stream, args);
           else
@@ -1662,6 +1584,8 @@ static size_t group_ws(const kfac_factor_job* jobs, int njobs) {
   plan_jobs(jobs, njobs, plans);
   size_t off = 0;
   for (int i = 0; i < njobs; ++i) off += plans[i].slab_bytes;
+  if (syrk3_group(jobs, njobs))
+    for (int i = 0; i < njobs; ++i) off += split3_bytes(jobs[i]);
   return off;
 }
 
