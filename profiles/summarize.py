@@ -58,8 +58,9 @@ def main(tag):
         note = ("FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->bytes, "
                 "mean over the bench's launches (15 updates per pass, last batch short)")
         if kname == "kfac_factor_syrk3":
-            note += ("; syrk3's panel loads are 4 B/lane buffer loads, for which the x2 is "
-                     "uncalibrated (MI355X_MICROARCH.md): fetch is an upper bound, x1 the lower")
+            note += ("; kfac_factor_syrk3 reads the split pass's bf16x3 panel images "
+                     "(6 B per operand element) by global_load_lds_dwordx4 (16 B/lane: the x2 "
+                     "applies); the split pass (kfac_split3) is a separate launch")
         out = {"kernel": kname, "tag": tag, "fetch_bytes_per_launch": fetch,
                "write_bytes_per_launch": write, "hbm_bytes_per_launch": fetch + write,
                "rocprof_trace": stats.get(kname), "note": note}
