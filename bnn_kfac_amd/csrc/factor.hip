@@ -750,8 +750,12 @@ struct ConvGeom {
   int units;       // workgroups per K-split (mode 0: ceil(nq / (4*CONV_CB)) block groups; else 1)
 };
 
-template <int LAYOUT, int PMAXE, bool STRIDE1, int CB = CONV_CB>
-__global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args, ConvGeom cg) {
+#ifndef KFAC_CONV_OCC
+#define KFAC_CONV_OCC 4  // resident workgroups per CU the mode-0 instances are compiled for
+#endif
+template <int LAYOUT, int PMAXE, bool STRIDE1, int CB = CONV_CB, bool M3 = false>
+__global__ __launch_bounds__(NTHREADS, (CB == 2 && !M3) ? KFAC_CONV_OCC : 4) void kfac_factor_conv(
+    FactorArgs args, ConvGeom cg) {
   extern __shared__ __attribute__((aligned(16))) float cimg[];
   const int task = xcd_task(blockIdx.x, gridDim.x);
   int jx = 0;
@@ -764,8 +768,11 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args,
   // nmine, the row groups) is then wave-uniform (scalar branches, no exec-mask
   // juggling around the operand reads of the MFMA chain)
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int mode = cg.mode;
-  const int klane = mode == 2 ? lane >> 4 : lane >> 5;
+  // M3: the mode-3 instance (its three accumulators and operand rings stay out of the
+  // other modes' register budget)
+  const int mode = M3 ? 3 : cg.mode;
+  const bool m16 = mode >= 2;  // 16x16x4 MFMA modes (2: one block; 3: blocks 00, 10, 11)
+  const int klane = m16 ? lane >> 4 : lane >> 5;
   const int64_t b0 = (int64_t)split * cg.B / J.splits, b1 = (int64_t)(split + 1) * cg.B / J.splits;
 
   // staging map: source element (PATCH) / float4 (CHANNEL) q of this thread -> LDS index
@@ -824,7 +831,7 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args,
   // (b = tri index), 4*CB per workgroup (unit), block b = unit*4*CB + wave + 4i: the
   // workgroup stages each image once for all its blocks and the waves' shares differ
   // by at most one block.  Narrow modes: the one block, every wave.
-  const int cl = mode == 2 ? lane & 15 : lane & 31;
+  const int cl = m16 ? lane & 15 : lane & 31;
   int offA[CB], offB[CB], bij[CB];
   bool same[CB];
   int nmine = 0;
@@ -835,20 +842,21 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args,
     if (mode == 0) tri_decode(bidx, bi, bj);
     const bool mine = mode ? i == 0 : bidx < cg.nq;
     nmine += mine;
-    offA[i] = column(32 * bi + cl);
+    // mode 3: offA[0] / offA[1] = feature columns 0..15 / 16..31 (both operands)
+    offA[i] = column(mode == 3 ? 16 * i + cl : 32 * bi + cl);
     offB[i] = column(32 * bj + cl);
     same[i] = bi == bj;
     bij[i] = (bi << 16) | bj;
   }
 
   floatx16 acc[CB];
-  floatx4 acc16;
+  floatx4 acc16, acc16b, acc16c;  // mode 2: block 00; mode 3: blocks 00, 10, 11
 #pragma unroll
   for (int i = 0; i < CB; ++i)
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[i][v] = 0.f;
 #pragma unroll
-  for (int v = 0; v < 4; ++v) acc16[v] = 0.f;
+  for (int v = 0; v < 4; ++v) acc16[v] = acc16b[v] = acc16c[v] = 0.f;
 
   // one row group of one block: T MFMAs, operands read two MFMAs ahead (LDS latency
   // off the accumulator chain)
@@ -916,9 +924,50 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args,
       }
     }
   };
+  // mode 3: features 0..15 (v0) and 16..31 (v1) of CK steps per chunk, double-
+  // buffered; each step feeds three 16x16x4 MFMAs (blocks 00 = v0 v0, 10 = v1 v0,
+  // 11 = v1 v1): two LDS reads per three MFMAs, where the 32x32 block of mode 1 took
+  // two per MFMA and computed the strictly-upper quarter too
+  auto row_mfmas3 = [&](const float* p0, const float* p1) {
+    constexpr int CK = 4;
+    const int st = STRIDE1 ? 1 : cg.stride, T = cg.T, last = (T - 1) * st;
+    float c0[CK], c1[CK], n0[CK], n1[CK];
+#pragma unroll
+    for (int u = 0; u < CK; ++u) {
+      const int o = min(u * st, last);
+      c0[u] = p0[o];
+      c1[u] = p1[o];
+    }
+    for (int t0 = 0; t0 < T; t0 += CK) {
+#pragma unroll
+      for (int u = 0; u < CK; ++u) {
+        const int o = min((t0 + CK + u) * st, last);
+        n0[u] = p0[o];
+        n1[u] = p1[o];
+      }
+#pragma unroll
+      for (int u = 0; u < CK; ++u) {
+        if (t0 + u < T) {
+          acc16 = __builtin_amdgcn_mfma_f32_16x16x4f32(c0[u], c0[u], acc16, 0, 0, 0);
+          acc16b = __builtin_amdgcn_mfma_f32_16x16x4f32(c1[u], c0[u], acc16b, 0, 0, 0);
+          acc16c = __builtin_amdgcn_mfma_f32_16x16x4f32(c1[u], c1[u], acc16c, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < CK; ++u) {
+        c0[u] = n0[u];
+        c1[u] = n1[u];
+      }
+    }
+  };
   // one row group of every block of this wave (rowA / rowB: LDS offsets added to the
   // blocks' column offsets; zeroA: A read from the zero plane)
   auto blocks = [&](int rowA, int rowB, bool zeroA) {
+    if constexpr (M3) {  // both operands from the same reads: a row past Ho reads zeros
+      row_mfmas3(cimg + (zeroA ? cg.zero_base : offA[0] + rowA),
+                 cimg + (zeroA ? cg.zero_base : offA[CB - 1] + rowA));
+      return;
+    }
     if (mode == 2) {
       row_mfmas(cimg + (zeroA ? cg.zero_base : offA[0] + rowA), cimg + offB[0] + rowB, true,
                 [&](float a, float b) { acc16 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc16, 0, 0, 0); });
@@ -962,6 +1011,34 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_conv(FactorArgs args,
   float* out = J.slab + (size_t)split * TILE * TILE;  // narrow: tile 0
   if (mode == 1) {
     store_narrow(J, out, acc[0], cimg);
+    return;
+  }
+  if constexpr (M3) {  // sum the 4 waves' three 16x16 partials in wave order (deterministic)
+    __syncthreads();
+    if (wave > 0) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        cimg[((wave - 1) * 12 + v) * 64 + lane] = acc16[v];
+        cimg[((wave - 1) * 12 + 4 + v) * 64 + lane] = acc16b[v];
+        cimg[((wave - 1) * 12 + 8 + v) * 64 + lane] = acc16c[v];
+      }
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    const int rr = (lane >> 4) * 4, cc = lane & 15;
+#pragma unroll
+    for (int blk = 0; blk < 3; ++blk) {
+      const int bi = blk ? 1 : 0, bj = blk == 2 ? 1 : 0;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float t = blk == 0 ? acc16[v] : blk == 1 ? acc16b[v] : acc16c[v];
+#pragma unroll
+        for (int w = 0; w < 3; ++w) t += cimg[(w * 12 + blk * 4 + v) * 64 + lane];
+        float* at = &out[(16 * bi + rr + v) * TILE + 16 * bj + cc];
+        if (!J.accum) *at = t;
+        else *at = J.sbeta == 0.f ? J.alpha * t : fmaf(J.sbeta, *at, J.alpha * t);
+      }
+    }
     return;
   }
   if (mode == 2) {  // sum the 4 waves' 16x16 partials in wave order (deterministic)
@@ -1098,8 +1175,11 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
   const int n = o.cols + (o.has_ones ? 1 : 0);
   g = ConvGeom{};
   g.n = n;
-  g.mode = n <= 16 ? 2 : (n <= 32 ? 1 : 0);
-  g.KR = g.mode == 2 ? 4 : 2;
+#ifndef KFAC_CONV_NARROW32
+#define KFAC_CONV_NARROW32 3  // n in 17..32: 3 = three 16x16 blocks, 1 = one 32x32 block (A/B)
+#endif
+  g.mode = n <= 16 ? 2 : (n <= 32 ? KFAC_CONV_NARROW32 : 0);
+  g.KR = g.mode >= 2 ? 4 : 2;
   g.bseg = (int)(o.rows / o.L);
   g.B = (int)(nseg * g.bseg);
   int64_t lds;
@@ -1114,7 +1194,7 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
     if ((int64_t)o.C * o.H * o.W > CONV_SRC_MAX) return false;
     g.Wp = o.W + 2 * o.pw;
     g.plane = (o.H + 2 * o.ph) * g.Wp;
-    if (g.mode != 2) {
+    if (g.mode != 2) {  // (mode 3 too: its 16-lane groups read 16 consecutive columns)
       const int64_t Wp = pad_to(g.Wp, o.kw);
       const int64_t plane = pad_to((int64_t)(o.H + 2 * o.ph) * Wp, (int64_t)o.kh * o.kw);
       const int64_t need = o.C * plane + 2 * (int64_t)o.Ho * o.sh * Wp;
@@ -1139,7 +1219,7 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
       return false;
     const int segs = g.mode ? 4 * g.KR : g.KR;  // narrow: the 4 waves' segments too
     int Q = (int)cdiv(o.L, segs);
-    if (g.mode == 2) Q = (int)pad_to(Q, 16);
+    if (g.mode >= 2) Q = (int)pad_to(Q, 16);
     g.rowstep = Q;
     g.plane = (int)pad_to((int64_t)segs * Q, 1);
     g.T = Q;
@@ -1175,13 +1255,26 @@ static void launch_conv(const FactorArgs& args, const ConvGeom& g, int tasks, hi
   const size_t shmem = (size_t)g.lds * sizeof(float);
   const bool s1 = g.stride == 1;
   const int pm = (int)cdiv(g.src, NTHREADS);  // <= 8 by CONV_SRC_MAX
-#define KFAC_CONV_LAUNCH(PM, S1) \
-  hipLaunchKernelGGL((kfac_factor_conv<LAYOUT, PM, S1>), dim3(tasks), dim3(NTHREADS), shmem, stream, args, g)
-  if (pm <= 4) {
-    if (s1) KFAC_CONV_LAUNCH(4, true); else KFAC_CONV_LAUNCH(4, false);
-  } else {
-    if (s1) KFAC_CONV_LAUNCH(8, true); else KFAC_CONV_LAUNCH(8, false);
-  }
+  // one instance per mode class, so each gets its own register budget: mode 0 (CB
+  // blocks per wave), the one-block narrow modes 1 / 2 (CB = 1), mode 3
+#define KFAC_CONV_LAUNCH(PM, S1, CBV, M3) \
+  hipLaunchKernelGGL((kfac_factor_conv<LAYOUT, PM, S1, CBV, M3>), dim3(tasks), dim3(NTHREADS), shmem, stream, \
+                     args, g)
+#define KFAC_CONV_PICK(CBV, M3)                                                   \
+  do {                                                                            \
+    if (pm <= 4) {                                                                \
+      if (s1) KFAC_CONV_LAUNCH(4, true, CBV, M3); else KFAC_CONV_LAUNCH(4, false, CBV, M3); \
+    } else {                                                                      \
+      if (s1) KFAC_CONV_LAUNCH(8, true, CBV, M3); else KFAC_CONV_LAUNCH(8, false, CBV, M3); \
+    }                                                                             \
+  } while (0)
+  if (g.mode == 3)
+    KFAC_CONV_PICK(CONV_CB, true);
+  else if (g.mode != 0)
+    KFAC_CONV_PICK(1, false);
+  else
+    KFAC_CONV_PICK(CONV_CB, false);
+#undef KFAC_CONV_PICK
 #undef KFAC_CONV_LAUNCH
 }
 
@@ -1392,7 +1485,9 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
       // (the n <= 8 channel kernel: half the slots -- its per-task reduction is the
       // larger cost there: conv1 G 15.7 / 12.4 / 13.2 us at k = 1 / 2 / 4)
       const bool small = jobs[i].x.layout == KFAC_CHANNEL && cg.n <= 8 && !conv_small_off();
-      int k = (int)std::max<int64_t>(1, cdiv((int64_t)cg.units * cg.B, small ? slots / 2 : slots));
+      // (mode-0 instances are compiled for KFAC_CONV_OCC resident workgroups per CU)
+      const int64_t cslots = cg.mode == 0 ? (int64_t)KFAC_CONV_OCC * 256 : slots;
+      int k = (int)std::max<int64_t>(1, cdiv((int64_t)cg.units * cg.B, small ? cslots / 2 : cslots));
       static const int env_k = [] {
         const char* v = getenv("KFAC_CONV_K");
         return v ? atoi(v) : 0;

@@ -1,4 +1,7 @@
-"""Host-side cost of KFAC.update / invert on the MLP bench setup (GPU box)."""
+"""Host-side cost of KFAC.update / invert on a bench setup (GPU box).
+
+    python tools/host_overhead.py [mlp|lenet|wide]
+"""
 import cProfile
 import io
 import os
@@ -15,19 +18,22 @@ from bnn_kfac_amd.curvatures import KFAC  # noqa: E402
 
 def main():
     dev = torch.device("cuda:0")
-    specs = bench.CONFIGS["mlp"]
-    net = bench.build_model("mlp", dev)
-    layers = [m for m in net.modules() if isinstance(m, torch.nn.Linear)]
-    recs = bench.synthetic_records(specs, 60000, dev, seed=0)
+    config = sys.argv[1] if len(sys.argv) > 1 else "mlp"
+    B, images = bench.SHAPES[(config, 1)][:2]
+    specs = bench.CONFIGS[config]
+    net = bench.build_model(config, dev)
+    layers = [m for m in net.modules() if isinstance(m, (torch.nn.Linear, torch.nn.Conv2d))]
+    recs = bench.synthetic_records(specs, images, dev, seed=0)
     kfac = KFAC(net)
-    starts = list(range(0, 60000, 4096))
+    kfac.eager_verdict = False
+    starts = list(range(0, images, B))
 
     def one_pass():
         kfac.reset()
         for i in starts:
             for layer, (a, g) in zip(layers, recs):
-                kfac.record[layer] = [a[i:i + 4096], g[i:i + 4096]]
-            kfac.update(batch_size=4096)
+                kfac.record[layer] = [a[i:i + B], g[i:i + B]]
+            kfac.update(batch_size=B)
         kfac.invert(0.04, 200)
 
     for _ in range(3):
@@ -50,8 +56,8 @@ def main():
     for k in range(n_up):
         i = starts[k % len(starts)]
         for layer, (a, g) in zip(layers, recs):
-            kfac.record[layer] = [a[i:i + 4096], g[i:i + 4096]]
-        kfac.update(batch_size=4096)
+            kfac.record[layer] = [a[i:i + B], g[i:i + B]]
+        kfac.update(batch_size=B)
     t_host = (time.perf_counter() - t0) / n_up
     torch.cuda.synchronize()
     t_all = (time.perf_counter() - t0) / n_up
