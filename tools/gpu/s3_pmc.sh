@@ -3,12 +3,12 @@ set -u
 OUT=gpurun_out/s3pmc
 mkdir -p $OUT
 export TMPDIR=/tmp
-export KFAC_SYRK3=1
+# (the bf16x3 SYRK is the default for the wide factors)
 BENCH="python3 bench.py --config wide --steps 1 --warmup 1 --no-cpu-baseline --no-e2e --no-serial"
 for C in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA" \
          "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE"; do
   name=$(echo $C | cut -d' ' -f1)
-  timeout -k 10 -s KILL 240 rocprofv3 --pmc $C --kernel-include-regex "syrk3" --output-format csv \
+  timeout -k 10 -s KILL 240 rocprofv3 --pmc $C --kernel-include-regex "kfac_factor_syrk3" --output-format csv \
       -d $OUT/pmc_$name -o run -- $BENCH > $OUT/pmc_$name.log 2>&1
   rc=$?; echo "pmc $name rc=$rc"; [ $rc -le 2 ] || exit $rc
 done
