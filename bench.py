@@ -416,14 +416,17 @@ def main(argv=None):
     sync()
     comm["timing"] = False
     N.profile_enable(False)
-    tiles_ms, tiles_n = N.profile_read(N.PROF_FACTOR_TILES)
-    s3_ms, s3_n = N.profile_read(N.PROF_FACTOR_SYRK3)
-    # the dominant factor kernel: the bf16x3 SYRK takes launch groups with a factor of
-    # n >= 2048 (wide), the fp32-MFMA kernel the rest
-    syrk3 = s3_ms > tiles_ms
-    f32_ms = tiles_ms
-    if syrk3:
-        tiles_ms, tiles_n = s3_ms, s3_n
+    # the factor-product kernels: kfac_factor_tiles (fp32 MFMA), kfac_factor_syrk3
+    # (split pass + bf16x3 MFMA, launch groups with a factor of n >= 2048) and
+    # kfac_factor_tiles_x3 (bf16x3 MFMA, fp32 panels split in registers); the roofline
+    # line is the one that took the most time
+    prods = {name: N.profile_read(pid) for name, pid in
+             (("kfac_factor_tiles", N.PROF_FACTOR_TILES), ("kfac_factor_syrk3", N.PROF_FACTOR_SYRK3),
+              ("kfac_factor_tiles_x3", N.PROF_FACTOR_X3))}
+    prod_kernel = max(prods, key=lambda k: prods[k][0])
+    tiles_ms, tiles_n = prods[prod_kernel]
+    prods_ms = sum(v[0] for v in prods.values())
+    syrk3 = prod_kernel != "kfac_factor_tiles"
     red_ms, red_n = N.profile_read(N.PROF_FACTOR_REDUCE)
     inv_ms, inv_n = N.profile_read(N.PROF_INVERT)
     N.profile_reset()
@@ -445,7 +448,9 @@ def main(argv=None):
     roofline = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                 "frac": (achieved / peak) if achieved else None,
                 "traffic": load_traffic(args.config),
-                "kernel": "kfac_factor_syrk3" if syrk3 else "kfac_factor_tiles",
+                "kernel": prod_kernel,
+                # (the same rate against the fp32 MFMA peak, the basis of earlier rounds)
+                "frac_fp32_peak_basis": (achieved / MFMA_F32_PEAK_TFLOPS) if achieved else None,
                 "peak_basis": ("dense bf16 MFMA 2.5 PF / 6 products per fp32 product (fp32-equivalent)"
                                if syrk3 else "dense fp32 MFMA"),
                 "launches": tiles_n,
@@ -455,7 +460,7 @@ def main(argv=None):
                 "flops_per_launch": fpi * images * args.steps / max(tiles_n, 1),
                 "algorithmic_bytes_per_launch": bytes_per_image(specs) * images * args.steps
                                                 / max(tiles_n, 1)}
-    breakdown = {"factor_tiles_ms_per_step": (tiles_ms + (f32_ms if syrk3 else s3_ms)) / args.steps,
+    breakdown = {"factor_tiles_ms_per_step": prods_ms / args.steps,
                  "factor_reduce_ms_per_step": red_ms / args.steps,
                  "invert_ms_per_step": inv_ms / args.steps,
                  "allreduce_ms_per_step": allreduce_ms,

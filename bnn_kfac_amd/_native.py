@@ -21,7 +21,8 @@ KFAC_OK, KFAC_EINVAL, KFAC_ELAUNCH, KFAC_EWORKSPACE = 0, -1, -2, -3
 ROWMAJOR, CHANNEL, PATCH = 0, 1, 2
 OUT_INV_CHOL, OUT_INVERSE = 0, 1
 TRI_SYMMETRIC, TRI_LOWER = 0, 1
-PROF_FACTOR_TILES, PROF_FACTOR_REDUCE, PROF_INVERT, PROF_QUAD_TILES, PROF_FACTOR_SYRK3 = 0, 1, 2, 3, 4
+(PROF_FACTOR_TILES, PROF_FACTOR_REDUCE, PROF_INVERT, PROF_QUAD_TILES, PROF_FACTOR_SYRK3,
+ PROF_FACTOR_X3) = 0, 1, 2, 3, 4, 5
 
 c_i32, c_i64, c_f32, c_f64, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_void_p
 

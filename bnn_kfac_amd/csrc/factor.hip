@@ -98,6 +98,7 @@ struct StageCursor {
 // Narrow factors (n <= 32): the 4 waves hold partial sums of quadrant (0,0) over
 // disjoint K subsets; sum them through LDS in wave order (deterministic) and store
 // the quadrant.  `lds` is free (the caller's stage loop has ended with a barrier).
+template <int NW = 4>
 __device__ __forceinline__ void store_narrow(const FactorJobDev& J, float* out, floatx16& acc,
                                              float* lds) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -109,7 +110,7 @@ __device__ __forceinline__ void store_narrow(const FactorJobDev& J, float* out, 
   __syncthreads();
   if (wave != 0) return;
 #pragma unroll
-  for (int w = 0; w < 3; ++w)
+  for (int w = 0; w < NW - 1; ++w)
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[v] += lds[(w * 16 + v) * 64 + lane];
   put_partial(J, acc, [&](int v) { return &out[acc_row(v, lane) * TILE + (lane & 31)]; });
@@ -172,49 +173,49 @@ __device__ __forceinline__ void factor_task(const FactorJobDev& J, const float* 
 // ds_read_b32 halves read 32 consecutive dwords, conflict-free).  Chunks past the
 // last real column (bias ones column, tile padding) and rows past the range load
 // from a safe address and are overwritten with their fill value once landed.
-// GBK rows per stage; each thread owns NCH = GBK/16 of a panel's 16-byte chunks.
-template <int GBK>
+// GBK rows per stage; each thread of NW waves owns NCH = GBK/(4 NW) of a panel's
+// 16-byte chunks.
+template <int GBK, int NW = 4>
 struct GldsPanel {
-  static constexpr int NCH = GBK / 16;
+  static constexpr int NCH = GBK / (4 * NW);
+  // chunk i of wave w, lane l: row (w NCH + i) * 4 + (l >> 4), columns col .. col + 3
+  // with col = col0 + 4 (l & 15) -- the same columns for every chunk of the lane
   int64_t ld, kend;
-  int ch[NCH];       // this thread's 16-byte chunks of a panel (GBK x 16 chunks)
-  int col[NCH];      // first column of each chunk
-  bool real[NCH];    // chunk holds matrix data (else fill)
-  float4 fill[NCH];  // fill value of a non-real chunk (ones column -> 1)
+  int col, ones, lrow;
+  bool real;  // the lane's chunks hold matrix data (else fill: ones column -> 1)
   __device__ __forceinline__ void init(const OpDev& op, int col0, int w, int lane, int64_t k_end) {
     ld = op.ld; kend = k_end;
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      ch[i] = (w * NCH + i) * 64 + lane;
-      col[i] = col0 + (ch[i] & 15) * 4;
-      real[i] = col[i] < op.cols;
-      float f[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) f[q] = (col[i] + q == op.ones) ? 1.f : 0.f;
-      fill[i] = make_float4(f[0], f[1], f[2], f[3]);
-    }
+    col = col0 + (lane & 15) * 4;
+    real = col < op.cols;
+    ones = op.ones;
+    lrow = w * NCH * 4 + (lane >> 4);
   }
   // issue the LDS-DMA loads of rows [k, k+GBK) of the batch at `base` into `slot`
   __device__ __forceinline__ void issue(const float* base, int64_t k, float* slot, int w) const {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int64_t row = k + (ch[i] >> 4);
+      const int64_t row = k + lrow + 4 * i;
       const int64_t r = row < kend ? row : kend - 1;
-      const float* src = base + r * ld + (real[i] ? col[i] : 0);
+      const float* src = base + r * ld + (real ? col : 0);
       __builtin_amdgcn_global_load_lds(src, slot + (w * NCH + i) * 256, 16, 0, 0);
     }
   }
   // after landing: overwrite chunks that must not hold matrix data
   __device__ __forceinline__ void fixup(int64_t k, float* slot) const {
+    const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const bool okrow = k + (ch[i] >> 4) < kend;
-      if (!real[i] || !okrow) {
+      const bool okrow = k + lrow + 4 * i < kend;
+      if (!real || !okrow) {
         // inline asm: the explicit vm_wait already covers this lane's DMA; a plain
         // store would make the compiler drain every in-flight stage (vmcnt(0))
         typedef float f4v __attribute__((ext_vector_type(4)));
-        const f4v v = okrow ? f4v{fill[i].x, fill[i].y, fill[i].z, fill[i].w} : f4v{0.f, 0.f, 0.f, 0.f};
-        const uint32_t addr = (uint32_t)(uintptr_t)(slot + ch[i] * 4);
+        f4v v = {0.f, 0.f, 0.f, 0.f};
+        if (okrow) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = col + q == ones ? 1.f : 0.f;
+        }
+        const uint32_t addr = (uint32_t)(uintptr_t)(slot + ((lrow / 4 + i) * 64 + lane) * 4);
         asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
       }
     }
@@ -246,20 +247,24 @@ __device__ __forceinline__ void stage_barrier() {
 // Narrow row-major factors (n <= 32) whose rows are not 16-B aligned (the MLP's
 // 10-wide output gradient): operands go from global memory straight into the MFMA
 // registers, one stage ahead, so the glds-only launch (32 KB of LDS) takes them
-// too.  Wave w takes rows 8w..8w+7 of every 32-row stage (the 4 waves split K; the
-// store sums them), lane (rr, h) row 2*s2 + h, column rr (the ones column: 1).
+// too.  Of NW waves, wave w takes rows (BK/NW) w .. of every 32-row stage (the waves
+// split K; the store sums them), lane (rr, h) row 2*s2 + h, column rr (the ones
+// column: 1).
+template <int NW = 4>
 __device__ __forceinline__ void narrow_direct_load(const FactorJobDev& J, const float* base, int64_t k0,
-                                                   float (&v)[BK / 8]) {
+                                                   float (&v)[BK / (2 * NW)]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, rr = lane & 31, h = lane >> 5;
 #pragma unroll
-  for (int s2 = 0; s2 < BK / 8; ++s2) {
-    const int64_t k = k0 + 2 * (wave * (BK / 8) + s2) + h;
+  for (int s2 = 0; s2 < BK / (2 * NW); ++s2) {
+    const int64_t k = k0 + 2 * (wave * (BK / (2 * NW)) + s2) + h;
     v[s2] = k < J.x.rows ? (rr < J.x.cols ? base[k * J.x.ld + rr] : (rr == J.x.ones ? 1.f : 0.f)) : 0.f;
   }
 }
 
+template <int NW = 4>
 __device__ __forceinline__ void factor_task_narrow_direct(const FactorJobDev& J, const float* const* segs,
                                                           int local, float* lds) {
+  constexpr int NV = BK / (2 * NW);
   const int split = local;  // one tile
   const int64_t s0 = (int64_t)split * J.chunk;
   const int64_t s1 = min(J.nst, s0 + J.chunk);
@@ -270,23 +275,23 @@ __device__ __forceinline__ void factor_task_narrow_direct(const FactorJobDev& J,
     StageCursor c;
     c.init(J, s0);
     const float* base = seg_base(J, segs, c.seg);
-    float cur[BK / 8], nxt[BK / 8];
-    narrow_direct_load(J, base, c.k, cur);
+    float cur[NV], nxt[NV];
+    narrow_direct_load<NW>(J, base, c.k, cur);
     for (int64_t s = s0; s < s1; ++s) {
       const int seg = c.seg;
       c.next(J.x.rows);
       if (s + 1 < s1) {
         if (c.seg != seg) base = seg_base(J, segs, c.seg);
-        narrow_direct_load(J, base, c.k, nxt);
+        narrow_direct_load<NW>(J, base, c.k, nxt);
       }
 #pragma unroll
-      for (int s2 = 0; s2 < BK / 8; ++s2)
+      for (int s2 = 0; s2 < NV; ++s2)
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[s2], cur[s2], acc, 0, 0, 0);
 #pragma unroll
-      for (int s2 = 0; s2 < BK / 8; ++s2) cur[s2] = nxt[s2];
+      for (int s2 = 0; s2 < NV; ++s2) cur[s2] = nxt[s2];
     }
   }
-  store_narrow(J, J.slab + (size_t)split * TILE * TILE, acc, lds);
+  store_narrow<NW>(J, J.slab + (size_t)split * TILE * TILE, acc, lds);
 }
 
 // NSLOT ring slots (2: one stage in flight, 4 WGs/CU); one barrier per stage.
@@ -700,6 +705,206 @@ __global__ __launch_bounds__(NTHREADS, S3D_WGS) void kfac_factor_syrk3(FactorArg
     factor_task_narrow_direct(J, args.segs, local, reinterpret_cast<float*>(s3lds));
   else
     s3d_task(J, local, s3lds);
+}
+
+// ------------------------------- fp32 panels, bf16x3 products split in registers
+// kfac_factor_tiles_x3: kfac_factor_tiles' LDS-DMA ring of fp32 32-row stages,
+// consumed by TWO waves per 64 x 64 tile, each computing the WHOLE tile over its
+// own 16-row half of every stage.  A lane reads 8 k of one column (its MFMA
+// fragment), splits them in registers (split3: the exact three-part split of the
+// bf16x3 kernels above) and the wave runs six v_mfma_f32_32x32x16_bf16 per 32 x 32
+// block: 24 MFMAs of 32 cycles per wave and 16-row half against the fp32 kernel's
+// 4 waves x 8 fp32 MFMAs of 64 cycles for the same work, with no split pass and no
+// padded images (the n <= 1024 factors, where kfac_split3's HBM round trip costs
+// as much as the products).  The two waves' partial tiles are summed through LDS
+// in a fixed order at the end.
+constexpr int X3_THREADS = 128;
+constexpr int X3_NW = X3_THREADS / 64;
+
+struct X3Frag {
+  bf16x8 p[3];  // hi, mid, lo
+};
+
+// lane's fragment: 8 consecutive k (rows, TILE floats apart) of one column
+__device__ __forceinline__ X3Frag x3_frag(const float* p) {
+  float x[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) x[r] = p[r * TILE];
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 h, m, l;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint32_t a, b, c;
+    split3(x[2 * i], x[2 * i + 1], a, b, c);
+    h[i] = a;
+    m[i] = b;
+    l[i] = c;
+  }
+  X3Frag f;
+  f.p[0] = __builtin_bit_cast(bf16x8, h);
+  f.p[1] = __builtin_bit_cast(bf16x8, m);
+  f.p[2] = __builtin_bit_cast(bf16x8, l);
+  return f;
+}
+
+__device__ __forceinline__ void x3_six(floatx16& acc, const X3Frag& A, const X3Frag& B) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.p[2], B.p[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.p[1], B.p[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.p[0], B.p[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.p[1], B.p[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.p[0], B.p[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.p[0], B.p[0], acc, 0, 0, 0);
+}
+
+// MASK bit 2 bi + bj: block (bi, bj) of the tile has work (lower triangle, inside
+// the factor); the stage loop is specialised per mask, so its body is straight-line
+// code the scheduler can interleave (loads / splits of one block under the MFMAs of
+// the previous).  Diagonal tiles read the A panel for B (the B panel is not loaded).
+template <int GBK, int NSLOT, int MASK>
+__device__ __forceinline__ void x3_loop(const FactorJobDev& J, const float* const* segs, int ti, int tj,
+                                        int64_t s0, int64_t s1, float* lds, floatx16 (&acc)[2][2]) {
+  constexpr bool A00 = MASK & 1, A01 = MASK & 2, A10 = MASK & 4, A11 = MASK & 8;
+  constexpr bool ROW1 = A10 || A11, COL1 = A01 || A11;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool same = ti == tj;
+  constexpr int GSLOT = 2 * GBK * TILE;
+  const int64_t rows = J.x.rows;
+  GldsPanel<GBK, X3_NW> pa, pb;
+  pa.init(J.x, ti * TILE, wave, lane, rows);
+  pb.init(J.x, tj * TILE, wave, lane, rows);
+  const int ns = (int)(s1 - s0);
+  const int per = (same ? 1 : 2) * GldsPanel<GBK, X3_NW>::NCH;
+  StageCursor ic, fc;
+  ic.init(J, s0);
+  fc = ic;
+  const float* ibase = seg_base(J, segs, ic.seg);
+  auto issue = [&](int sl) {
+    float* slot = lds + (sl % NSLOT) * GSLOT;
+    pa.issue(ibase, ic.k, slot, wave);
+    if (!same) pb.issue(ibase, ic.k, slot + GBK * TILE, wave);
+    const int seg = ic.seg;
+    ic.next(rows);
+    if (ic.seg != seg && sl + 1 < ns) ibase = seg_base(J, segs, ic.seg);
+  };
+#pragma unroll
+  for (int p0 = 0; p0 < NSLOT - 1; ++p0)
+    if (p0 < ns) issue(p0);
+  // lane's fragment base: column (lane & 31) of block 0, rows 16 wave + 8 (lane >> 5)
+  const int fo = (16 * wave + 8 * (lane >> 5)) * TILE + (lane & 31);
+  const int bo = fo + (same ? 0 : GBK * TILE);
+  for (int st = 0; st < ns; ++st) {
+    const int issued = min(ns - 1, st + NSLOT - 2);
+    vm_wait(per * (issued - st));
+    float* slot = lds + (st % NSLOT) * GSLOT;
+    pa.fixup(fc.k, slot);
+    if (!same) pb.fixup(fc.k, slot + GBK * TILE);
+    fc.next(rows);
+    stage_barrier();
+    if (st + NSLOT - 1 < ns) issue(st + NSLOT - 1);
+    const X3Frag A0 = x3_frag(slot + fo);
+    const X3Frag B0 = x3_frag(slot + bo);
+    if constexpr (A00) x3_six(acc[0][0], A0, B0);
+    if constexpr (ROW1) {
+      const X3Frag A1 = x3_frag(slot + fo + 32);
+      if constexpr (A10) x3_six(acc[1][0], A1, B0);
+      if constexpr (COL1) {
+        const X3Frag B1 = x3_frag(slot + bo + 32);
+        if constexpr (A01) x3_six(acc[0][1], A0, B1);
+        if constexpr (A11) x3_six(acc[1][1], A1, B1);
+      }
+    } else if constexpr (COL1) {
+      const X3Frag B1 = x3_frag(slot + bo + 32);
+      x3_six(acc[0][1], A0, B1);
+    }
+  }
+}
+
+template <int GBK, int NSLOT>
+__device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const float* const* segs, int local,
+                                               float* lds, int split_major) {
+  static_assert(GBK == 16 * X3_NW, "one 16-row half stage per wave");
+  const int ntiles = J.t * (J.t + 1) / 2;
+  const int split = split_major ? local / ntiles : local % J.splits;
+  const int tile = split_major ? local - split * ntiles : local / J.splits;
+  int ti, tj;
+  tri_decode(tile, ti, tj);
+  const int64_t s0 = (int64_t)split * J.chunk;
+  const int64_t s1 = min(J.nst, s0 + J.chunk);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool same = ti == tj;
+  bool act[2][2];
+  int mask = 0;
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj) {
+      act[bi][bj] = !(same && bi < bj) && ti * TILE + bi * 32 < J.n && tj * TILE + bj * 32 < J.n;
+      mask |= act[bi][bj] << (2 * bi + bj);
+    }
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[bi][bj][v] = 0.f;
+  if (s1 > s0) {
+    switch (mask) {  // (block (0, 0) always has work)
+      case 15: x3_loop<GBK, NSLOT, 15>(J, segs, ti, tj, s0, s1, lds, acc); break;
+      case 13: x3_loop<GBK, NSLOT, 13>(J, segs, ti, tj, s0, s1, lds, acc); break;  // diagonal
+      case 5: x3_loop<GBK, NSLOT, 5>(J, segs, ti, tj, s0, s1, lds, acc); break;
+      case 3: x3_loop<GBK, NSLOT, 3>(J, segs, ti, tj, s0, s1, lds, acc); break;
+      case 1: x3_loop<GBK, NSLOT, 1>(J, segs, ti, tj, s0, s1, lds, acc); break;
+      default: x3_loop<GBK, NSLOT, 15>(J, segs, ti, tj, s0, s1, lds, acc); break;  // (not reached)
+    }
+  }
+  // wave w stores block row w: it hands the other block row's partials to the other
+  // wave through LDS (the ring is free after the barrier), then adds the other
+  // wave's.  Both sums are w0 + w1 (IEEE addition commutes): deterministic.
+  __syncthreads();
+  float* xo = lds;  // [wave][bj][16 values][64 lanes]
+  float* out = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE;
+  auto hand = [&](auto bic) {
+    constexpr int bi = decltype(bic)::value;
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+      if (act[bi][bj])
+#pragma unroll
+        for (int v = 0; v < 16; ++v) xo[((wave * 2 + bj) * 16 + v) * 64 + lane] = acc[bi][bj][v];
+  };
+  auto keep = [&](auto bic) {
+    constexpr int bi = decltype(bic)::value;
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+      if (act[bi][bj]) {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[bi][bj][v] += xo[(((1 - wave) * 2 + bj) * 16 + v) * 64 + lane];
+        put_partial(J, acc[bi][bj],
+                    [&](int v) { return &out[(bi * 32 + acc_row(v, lane)) * TILE + bj * 32 + (lane & 31)]; });
+      }
+  };
+  if (wave == 0) hand(std::integral_constant<int, 1>{});
+  else hand(std::integral_constant<int, 0>{});
+  __syncthreads();
+  if (wave == 0) keep(std::integral_constant<int, 0>{});
+  else keep(std::integral_constant<int, 1>{});
+}
+
+// Every job of the launch is LDS-DMA-eligible or narrow (n <= 32: direct loads).
+__global__ __launch_bounds__(X3_THREADS, 3) void kfac_factor_tiles_x3(FactorArgs args) {
+  __shared__ __attribute__((aligned(16))) float lds[2 * 2 * BK * TILE];
+  for (int i = 0; i < args.stagger * (int)(blockIdx.x >> 8); ++i) __builtin_amdgcn_s_sleep(8);
+  const int task = xcd_task(blockIdx.x, gridDim.x);
+  int j = 0;
+  while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
+  const FactorJobDev& J = args.job[j];
+  const int local = task - J.task_begin;
+  if (J.n <= 32)
+    factor_task_narrow_direct<X3_NW>(J, args.segs, local, lds);
+  else
+    factor_task_x3<BK, 2>(J, args.segs, local, lds, args.split_major);
 }
 
 // ------------------------------------------------------------ conv operands
@@ -1419,6 +1624,33 @@ static bool syrk3_group(const kfac_factor_job* jobs, int njobs) {
   return nmax > 32 && (mode == 1 || nmax >= 2048);
 }
 
+// kfac_factor_tiles_x3 (fp32 panels, bf16x3 products split in registers) for every
+// row-major group the split-pass kernel does not take (default; KFAC_TILES_X3=0: the
+// fp32-MFMA kfac_factor_tiles).  MNIST MLP, same box, 2 reps: 1.21-1.23e8 vs
+// 1.01e8 img/s, 81-82 vs 108 us per launch, the inversion beside the pass 0.41 vs
+// 0.61 ms (2 SYRK waves per SIMD instead of 4).  Groups whose largest factor has
+// n < 512 keep the fp32 kernel (LeNet-5's fully connected factors, n <= 401: 1.34e7
+// vs 1.39e7 img/s with x3).
+static int tiles_x3_mode() {
+  static const int m = [] {
+    const char* v = getenv("KFAC_TILES_X3");
+    return v && v[0] == '1' ? 1 : v && v[0] == '0' ? 0 : -1;
+  }();
+  return m;
+}
+
+static bool tiles_x3_group(const kfac_factor_job* jobs, int njobs) {
+  if (tiles_x3_mode() == 0 || njobs <= 0 || syrk3_group(jobs, njobs)) return false;
+  int nmax = 0;
+  for (int i = 0; i < njobs; ++i) {
+    if (jobs[i].x.layout != KFAC_ROWMAJOR) return false;
+    const int n = factor_n(jobs[i]);
+    if (n > 32 && !job_glds(jobs[i])) return false;
+    nmax = std::max(nmax, n);
+  }
+  return nmax >= (tiles_x3_mode() == 1 ? 33 : 512);
+}
+
 static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
                       int64_t slots = 0) {
   const bool s3 = syrk3_group(jobs, njobs);
@@ -1628,8 +1860,9 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
   const int tasks = g.tasks, rtiles = g.rtiles;
   if (tasks == 0) return KFAC_OK;
   const bool s3 = syrk3_group(jobs, njobs);
+  const bool x3 = tiles_x3_group(jobs, njobs);
   {
-    ProfScope ps(s3 ? KFAC_PROF_FACTOR_SYRK3 : KFAC_PROF_FACTOR_TILES, stream);
+    ProfScope ps(s3 ? KFAC_PROF_FACTOR_SYRK3 : x3 ? KFAC_PROF_FACTOR_X3 : KFAC_PROF_FACTOR_TILES, stream);
     // launch_groups() gives every channel-major / im2col job a group of its own
     // conv jobs whose images fit LDS: the image-staged kernel
     ConvGeom cg;
@@ -1661,7 +1894,9 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
               KFAC_CHECK_LAUNCH();
             }
             hipLaunchKernelGGL(kfac_factor_syrk3, dim3(tasks), dim3(NTHREADS), S3D_LDS, stream, args);
-          } else if (all_glds)
+          } else if (x3)
+            hipLaunchKernelGGL(kfac_factor_tiles_x3, dim3(tasks), dim3(X3_THREADS), 0, stream, args);
+          else if (all_glds)
             hipLaunchKernelGGL(kfac_factor_tiles_glds, dim3(tasks), dim3(NTHREADS), 0, stream, args);
           else
             hipLaunchKernelGGL(kfac_factor_tiles, dim3(tasks), dim3(NTHREADS), 0, stream, args);

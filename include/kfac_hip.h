@@ -313,11 +313,14 @@ KFAC_API int kfac_tri_unpack(const kfac_tri_job* jobs, int njobs, const float* p
  * Optional HIP-event timing of the library's own launches, recorded on the
  * stream each kernel is launched on (off by default; not graph-capturable when
  * on).  Kernel ids: 0 factor tiles (fp32-MFMA SYRK), 1 factor reduce, 2 whole
- * invert call, 3 quadform tiles, 4 factor tiles by the bf16x3 SYRK (launch groups
- * whose largest factor has n >= 2048, or KFAC_SYRK3=1).  kfac_profile_read syncs
- * the recorded events.                                                       */
+ * invert call, 3 quadform tiles, 4 factor tiles by the split-pass bf16x3 SYRK
+ * (launch groups whose largest factor has n >= 2048, or KFAC_SYRK3=1; the split
+ * pass included), 5 factor tiles by the bf16x3 SYRK that splits fp32 panels in
+ * registers (kfac_factor_tiles_x3).  kfac_profile_read syncs the recorded
+ * events.                                                                    */
 enum kfac_prof_id { KFAC_PROF_FACTOR_TILES = 0, KFAC_PROF_FACTOR_REDUCE = 1, KFAC_PROF_INVERT = 2,
-                    KFAC_PROF_QUAD_TILES = 3, KFAC_PROF_FACTOR_SYRK3 = 4, KFAC_PROF_COUNT = 5 };
+                    KFAC_PROF_QUAD_TILES = 3, KFAC_PROF_FACTOR_SYRK3 = 4, KFAC_PROF_FACTOR_X3 = 5,
+                    KFAC_PROF_COUNT = 6 };
 KFAC_API int kfac_profile_enable(int on);
 KFAC_API int kfac_profile_read(int id, double* total_ms, int64_t* launches);
 KFAC_API int kfac_profile_reset(void);
