@@ -1,0 +1,16 @@
+# x3 SYRK: per-wave DMA rings (no barrier in the loop; default build) vs one shared
+# ring (libkfac_hip_x3s.so, KFAC_X3_WAVE_RING=0); parity of the default first
+set -o pipefail
+mkdir -p gpurun_out/x3r
+KFAC_TILES_X3=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_factors.py tests/test_gpu_c3.py tests/test_gpu_invert.py tests/test_gpu_golden_r02.py tests/test_gpu_wide.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/x3r/tests.log 2>&1 || { tail -40 gpurun_out/x3r/tests.log; exit 1; }
+tail -1 gpurun_out/x3r/tests.log
+show() { python -c "
+import json; d=json.loads(open('$1').read().strip().splitlines()[-1]); b=d['breakdown']; r=d['roofline']
+print('$1', '%.4g'%d['value'], 'ms/step %.3f'%d['ms_per_step'], 'tiles %.3f'%b['factor_tiles_ms_per_step'], 'inv %.3f'%b['invert_ms_per_step'], r['kernel'], 'avg_us %.1f'%r['avg_launch_us'], 'frac %.3f'%r['frac'], 'serial %.4g'%(d.get('serial_images_per_s') or 0))"; }
+for r in 1 2; do
+for L in wave shared; do
+  LIB=$PWD/bnn_kfac_amd/libkfac_hip.so; [ $L = shared ] && LIB=$PWD/bnn_kfac_amd/libkfac_hip_x3s.so
+  BNN_KFAC_AMD_LIB=$LIB timeout -k 10 200 python bench.py --no-cpu-baseline --no-e2e > gpurun_out/x3r/mlp_${L}_$r.log 2>&1 || exit 1
+  show gpurun_out/x3r/mlp_${L}_$r.log
+done
+done
