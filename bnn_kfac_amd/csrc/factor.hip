@@ -718,70 +718,30 @@ __global__ __launch_bounds__(NTHREADS, S3D_WGS) void kfac_factor_syrk3(FactorArg
     s3d_task(J, local, s3lds);
 }
 
-// ------------------------------- fp32 panels, bf16x3 products split in registers
-// kfac_factor_tiles_x3: kfac_factor_tiles' LDS-DMA ring of fp32 32-row stages,
-// consumed by TWO waves per 64 x 64 tile, each computing the WHOLE tile over its
-// own 16-row half of every stage.  A lane reads 8 k of one column (its MFMA
-// fragment), splits them in registers (split3: the exact three-part split of the
-// bf16x3 kernels above) and the wave runs six v_mfma_f32_32x32x16_bf16 per 32 x 32
-// block: 24 MFMAs of 32 cycles per wave and 16-row half against the fp32 kernel's
-// 4 waves x 8 fp32 MFMAs of 64 cycles for the same work, with no split pass and no
-// padded images (the n <= 1024 factors, where kfac_split3's HBM round trip costs
-// as much as the products).  The two waves' partial tiles are summed through LDS
-// in a fixed order at the end.
+// ------------------------------- fp32 operands, bf16x3 products split in registers
+// kfac_factor_tiles_x3: TWO waves per 64 x 64 tile, each computing the WHOLE tile over
+// its own 16-row half of every 32-row stage.  A lane loads its MFMA fragment -- 8
+// consecutive k of one column -- straight from global memory into registers (no LDS),
+// splits it (split3: the exact three-part split of the bf16x3 kernels above) and the
+// wave runs six v_mfma_f32_32x32x16_bf16 per 32 x 32 block: 24 MFMAs of 32 cycles per
+// wave and 16-row half, against the fp32 kernel's 4 waves x 8 fp32 MFMAs of 64 cycles
+// for the same work, with no split pass and no padded images (the n <= 1024 factors,
+// where kfac_split3's HBM round trip costs as much as the products).  The two waves'
+// partial tiles are summed through LDS in a fixed order at the end.
+// Measured on the MNIST MLP group (profiles/r03_x3/ab/probe_summary.txt): direct loads
+// beat LDS-DMA rings (shared, one barrier per stage, or one per wave without a
+// barrier: 179 vs 196-204 us per 32,768-row launch), the compiled split beats a
+// hand-ordered asm one, and 128 x 128 macro tiles with the split made once per macro
+// tile into the syrk3 LDS image (x3m) lost (224 us).  The kernel is issue-bound: two
+// waves per SIMD keep its issue port ~90 % busy with 7.3 split VALU per MFMA.
 constexpr int X3_THREADS = 128;
-#ifndef KFAC_X3_PROBE
-#define KFAC_X3_PROBE 0  // timing probes (tools/x3_probe.py): 1 no DMA, 2 no split, 3 no MFMA
-#endif
-#ifndef KFAC_X3_DIRECT
-#define KFAC_X3_DIRECT 1  // operands by buffer loads straight into registers (else LDS-DMA rings)
-#endif
-#ifndef KFAC_X3_WAVE_RING
-#define KFAC_X3_WAVE_RING 1  // per-wave DMA rings, no barrier in the loop (else: a shared ring)
-#endif
 constexpr int X3_NW = X3_THREADS / 64;
 
 struct X3Frag {
   bf16x8 p[3];  // hi, mid, lo
 };
 
-// lane's fragment: 8 consecutive k (rows, TILE floats apart) of one column
-__device__ __forceinline__ X3Frag x3_frag(const float* p) {
-  float x[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) x[r] = p[r * TILE];
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  u32x4 h, m, l;
-#if KFAC_X3_PROBE == 2  // (timing probe: no split, the raw bits as parts)
-  X3Frag g;
-  g.p[0] = __builtin_bit_cast(bf16x8, u32x4{__float_as_uint(x[0]), __float_as_uint(x[1]), __float_as_uint(x[2]), __float_as_uint(x[3])});
-  g.p[1] = __builtin_bit_cast(bf16x8, u32x4{__float_as_uint(x[4]), __float_as_uint(x[5]), __float_as_uint(x[6]), __float_as_uint(x[7])});
-  g.p[2] = g.p[0];
-  return g;
-#endif
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    uint32_t a, b, c;
-    split3(x[2 * i], x[2 * i + 1], a, b, c);
-    h[i] = a;
-    m[i] = b;
-    l[i] = c;
-  }
-  X3Frag f;
-  f.p[0] = __builtin_bit_cast(bf16x8, h);
-  f.p[1] = __builtin_bit_cast(bf16x8, m);
-  f.p[2] = __builtin_bit_cast(bf16x8, l);
-  return f;
-}
-
 __device__ __forceinline__ void x3_six(floatx16& acc, const X3Frag& A, const X3Frag& B) {
-#if KFAC_X3_PROBE == 3  // (timing probe: no MFMA; the parts folded into one value)
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  u32x4 t = __builtin_bit_cast(u32x4, A.p[0]) ^ __builtin_bit_cast(u32x4, A.p[1]) ^ __builtin_bit_cast(u32x4, A.p[2]) ^
-            __builtin_bit_cast(u32x4, B.p[0]) ^ __builtin_bit_cast(u32x4, B.p[1]) ^ __builtin_bit_cast(u32x4, B.p[2]);
-  acc[0] += __uint_as_float(t[0] ^ t[1] ^ t[2] ^ t[3]);
-  return;
-#endif
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.p[2], B.p[0], acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.p[1], B.p[1], acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.p[0], B.p[2], acc, 0, 0, 0);
@@ -790,112 +750,6 @@ __device__ __forceinline__ void x3_six(floatx16& acc, const X3Frag& A, const X3F
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.p[0], B.p[0], acc, 0, 0, 0);
 }
 
-// MASK bit 2 bi + bj: block (bi, bj) of the tile has work (lower triangle, inside
-// the factor); the stage loop is specialised per mask, so its body is straight-line
-// code the scheduler can interleave (loads / splits of one block under the MFMAs of
-// the previous).  Diagonal tiles read the A panel for B (the B panel is not loaded).
-template <int GBK, int NSLOT, int MASK>
-__device__ __forceinline__ void x3_loop(const FactorJobDev& J, const float* const* segs, int ti, int tj,
-                                        int64_t s0, int64_t s1, float* lds, floatx16 (&acc)[2][2]) {
-  constexpr bool A00 = MASK & 1, A01 = MASK & 2, A10 = MASK & 4, A11 = MASK & 8;
-  constexpr bool ROW1 = A10 || A11, COL1 = A01 || A11;
-  // masks 13 and 1 occur on diagonal tiles only (an off-diagonal tile with block
-  // (1, 1) or any block has (0, 1)): B fragments = A fragments
-  constexpr bool SAME = MASK == 13 || MASK == 1;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool same = ti == tj;
-  const int64_t rows = J.x.rows;
-  const int ns = (int)(s1 - s0);
-  StageCursor ic, fc;
-  ic.init(J, s0);
-  fc = ic;
-  const float* ibase = seg_base(J, segs, ic.seg);
-#if KFAC_X3_WAVE_RING
-  // Each wave streams ITS 16 rows of every stage into a ring of its own (NSLOT slots
-  // of A and B 16 x 64 panels, 8 KB each) and waits only on its own DMA: no barrier
-  // in the loop, the two waves run free of each other.
-  constexpr int HR = GBK / X3_NW;     // rows per wave per stage (16)
-  constexpr int WSLOT = 2 * HR * TILE;  // floats per wave slot
-  float* ring = lds + wave * NSLOT * WSLOT;
-  GldsPanel<HR, 1> pa, pb;
-  pa.init(J.x, ti * TILE, 0, lane, rows);
-  pb.init(J.x, tj * TILE, 0, lane, rows);
-  const int per = (same ? 1 : 2) * GldsPanel<HR, 1>::NCH;
-  auto issue = [&](int sl) {
-    float* slot = ring + (sl % NSLOT) * WSLOT;
-    pa.issue(ibase, ic.k + HR * wave, slot, 0);
-    if (!same) pb.issue(ibase, ic.k + HR * wave, slot + HR * TILE, 0);
-    const int seg = ic.seg;
-    ic.next(rows);
-    if (ic.seg != seg && sl + 1 < ns) ibase = seg_base(J, segs, ic.seg);
-  };
-#pragma unroll
-  for (int p0 = 0; p0 < NSLOT - 1; ++p0)
-    if (p0 < ns) issue(p0);
-  const int fo = 8 * (lane >> 5) * TILE + (lane & 31);
-  const int bo = fo + (same ? 0 : HR * TILE);
-  for (int st = 0; st < ns; ++st) {
-    float* slot = ring + (st % NSLOT) * WSLOT;
-#if KFAC_X3_PROBE != 1  // (timing probe 1: no DMA in the loop)
-    const int issued = min(ns - 1, st + NSLOT - 2);
-    vm_wait(per * (issued - st));
-    pa.fixup(fc.k + HR * wave, slot);
-    if (!same) pb.fixup(fc.k + HR * wave, slot + HR * TILE);
-    fc.next(rows);
-    // (this wave's reads of the slot the next DMA overwrites completed in the
-    // previous trip: their results were consumed there)
-    if (st + NSLOT - 1 < ns) issue(st + NSLOT - 1);
-#endif
-#else
-  constexpr int GSLOT = 2 * GBK * TILE;
-  GldsPanel<GBK, X3_NW> pa, pb;
-  pa.init(J.x, ti * TILE, wave, lane, rows);
-  pb.init(J.x, tj * TILE, wave, lane, rows);
-  const int per = (same ? 1 : 2) * GldsPanel<GBK, X3_NW>::NCH;
-  auto issue = [&](int sl) {
-    float* slot = lds + (sl % NSLOT) * GSLOT;
-    pa.issue(ibase, ic.k, slot, wave);
-    if (!same) pb.issue(ibase, ic.k, slot + GBK * TILE, wave);
-    const int seg = ic.seg;
-    ic.next(rows);
-    if (ic.seg != seg && sl + 1 < ns) ibase = seg_base(J, segs, ic.seg);
-  };
-#pragma unroll
-  for (int p0 = 0; p0 < NSLOT - 1; ++p0)
-    if (p0 < ns) issue(p0);
-  // lane's fragment base: column (lane & 31) of block 0, rows 16 wave + 8 (lane >> 5)
-  const int fo = (16 * wave + 8 * (lane >> 5)) * TILE + (lane & 31);
-  const int bo = fo + (same ? 0 : GBK * TILE);
-  for (int st = 0; st < ns; ++st) {
-    const int issued = min(ns - 1, st + NSLOT - 2);
-    vm_wait(per * (issued - st));
-    float* slot = lds + (st % NSLOT) * GSLOT;
-    pa.fixup(fc.k, slot);
-    if (!same) pb.fixup(fc.k, slot + GBK * TILE);
-    fc.next(rows);
-    stage_barrier();
-    if (st + NSLOT - 1 < ns) issue(st + NSLOT - 1);
-#endif
-    const X3Frag A0 = x3_frag(slot + fo);
-    const X3Frag B0 = SAME ? A0 : x3_frag(slot + bo);
-    if constexpr (A00) x3_six(acc[0][0], A0, B0);
-    if constexpr (ROW1) {
-      const X3Frag A1 = x3_frag(slot + fo + 32);
-      if constexpr (A10) x3_six(acc[1][0], A1, B0);
-      if constexpr (COL1) {
-        const X3Frag B1 = SAME ? A1 : x3_frag(slot + bo + 32);
-        if constexpr (A01) x3_six(acc[0][1], A0, B1);
-        if constexpr (A11) x3_six(acc[1][1], A1, B1);
-      }
-    } else if constexpr (COL1) {
-      const X3Frag B1 = x3_frag(slot + bo + 32);
-      x3_six(acc[0][1], A0, B1);
-    }
-  }
-}
-
-#if KFAC_X3_DIRECT
 // Operands straight from global memory into registers, no LDS: a lane's fragment is
 // rows kw .. kw+7 of one column, eight buffer loads that differ only in their SGPR
 // offset (r * ld * 4 bytes), so the addressing costs no VALU; the buffer's record
@@ -939,7 +793,9 @@ __device__ __forceinline__ void x3_loop_direct(const FactorJobDev& J, const floa
                                                int64_t s0, int64_t s1, floatx16 (&acc)[2][2]) {
   constexpr bool A00 = MASK & 1, A01 = MASK & 2, A10 = MASK & 4, A11 = MASK & 8;
   constexpr bool ROW1 = A10 || A11, COL1 = A01 || A11;
-  constexpr bool SAME = MASK == 13 || MASK == 1;  // diagonal tiles only (see x3_loop)
+  // masks 13 and 1 occur on diagonal tiles only (an off-diagonal tile with block
+  // (1, 1), or with any block, has (0, 1)): B fragments = A fragments
+  constexpr bool SAME = MASK == 13 || MASK == 1;
   // fragments: 0 A block 0, 1 A block 1, 2 B block 0, 3 B block 1
   constexpr bool USE[4] = {true, ROW1, !SAME, !SAME && COL1};
   const int lane = threadIdx.x & 63;
@@ -1013,8 +869,6 @@ __device__ __forceinline__ void x3_loop_direct(const FactorJobDev& J, const floa
     }
   }
 }
-#endif
-
 template <int GBK, int NSLOT>
 __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const float* const* segs, int local,
                                                float* lds, int split_major) {
@@ -1046,7 +900,6 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[bi][bj][v] = 0.f;
   if (s1 > s0) {
-#if KFAC_X3_DIRECT
     switch (mask) {  // (block (0, 0) always has work)
       case 15: x3_loop_direct<15>(J, segs, ti, tj, s0, s1, acc); break;
       case 13: x3_loop_direct<13>(J, segs, ti, tj, s0, s1, acc); break;  // diagonal
@@ -1055,16 +908,6 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
       case 1: x3_loop_direct<1>(J, segs, ti, tj, s0, s1, acc); break;
       default: x3_loop_direct<15>(J, segs, ti, tj, s0, s1, acc); break;  // (not reached)
     }
-#else
-    switch (mask) {  // (block (0, 0) always has work)
-      case 15: x3_loop<GBK, NSLOT, 15>(J, segs, ti, tj, s0, s1, lds, acc); break;
-      case 13: x3_loop<GBK, NSLOT, 13>(J, segs, ti, tj, s0, s1, lds, acc); break;  // diagonal
-      case 5: x3_loop<GBK, NSLOT, 5>(J, segs, ti, tj, s0, s1, lds, acc); break;
-      case 3: x3_loop<GBK, NSLOT, 3>(J, segs, ti, tj, s0, s1, lds, acc); break;
-      case 1: x3_loop<GBK, NSLOT, 1>(J, segs, ti, tj, s0, s1, lds, acc); break;
-      default: x3_loop<GBK, NSLOT, 15>(J, segs, ti, tj, s0, s1, lds, acc); break;  // (not reached)
-    }
-#endif
   }
   // wave w stores block row w: it hands the other block row's partials to the other
   // wave through LDS (the ring is free after the barrier), then adds the other
@@ -1098,154 +941,12 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
   else keep(std::integral_constant<int, 1>{});
 }
 
-#if KFAC_X3_DIRECT
-// ------------- bf16x3 SYRK on 128 x 128 macro tiles, split in the kernel (x3m)
-// kfac_factor_syrk3's macro tiles and LDS image (s3_consume_sub), but the images are
-// made in the kernel instead of by a split pass through HBM: per 16-row substep wave
-// w loads (buffer loads, one substep ahead) A-panel fragment w and B-panel fragment w
-// -- 32 columns x 8 k per lane -- splits them and writes their three parts into the
-// substep's slot; after the barrier every wave reads its 12 fragments and runs its 24
-// MFMAs.  Each element is split once per macro tile: 3.7 VALU per MFMA against x3's
-// 7.3 (64 x 64 per wave), the price the padding to 128 columns.
-constexpr int X3M_NSLOT = 2;
-// 2 slots = 49,280 B, declared as 56 KB so that at most 2 workgroups share a CU (a third
-// would fit 160 KB) and an overlapped inversion's 29 KB workgroup still does
-constexpr int X3M_LDS = 56 * 1024;
-static_assert(X3M_NSLOT * S3_REG <= X3M_LDS, "x3m ring exceeds its LDS");
-
-__device__ __forceinline__ void x3m_task(const FactorJobDev& J, const float* const* segs, int local, char* lds) {
-  const int T3 = (J.n + MT - 1) / MT, units = T3 * (T3 + 1) / 2;
-  const int split = local / units, unit = local - split * units;
-  int I, Jc;
-  s3_decode(unit, T3, I, Jc);
-  const bool same = I == Jc;
-  const int64_t s0 = (int64_t)split * J.chunk;
-  const int64_t s1 = min(J.nst, s0 + J.chunk);
-  const int ns = (int)(s1 - s0);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  bool act[2][2];
-#pragma unroll
-  for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj) {
-      const int r0 = I * MT + wr * 64 + bi * 32, c0 = Jc * MT + wc * 64 + bj * 32;
-      act[bi][bj] = r0 < J.n && c0 < J.n && r0 >= c0;
-    }
-  const bool any = act[0][0] || act[0][1] || act[1][0] || act[1][1];
-  floatx16 acc[2][2];
-#pragma unroll
-  for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[bi][bj][v] = 0.f;
-  const int cl = lane & 31, hh = lane >> 5;
-  const int lo = s3_half(cl, hh);
-  const int oa = wr * 64 * 32 + lo;
-  const int ob = ((same ? 0 : MT) + wc * 64) * 32 + lo;
-  // this wave's producer fragments: columns 32 wave + cl of the A and B panels
-  const int ld4 = (int)J.x.ld * 4;
-  const int64_t rows = J.x.rows;
-  const int ca = I * MT + 32 * wave, cb = Jc * MT + 32 * wave;
-  const bool useA = ca < J.n, useB = !same && cb < J.n;
-  X3Col colA, colB;
-  {
-    const int c = ca + cl, d = cb + cl;
-    colA.fill = c >= J.x.cols;
-    colA.fv = c == J.x.ones ? 1.f : 0.f;
-    colA.voff = 8 * hh * ld4 + (colA.fill ? 0 : c) * 4;
-    colB.fill = d >= J.x.cols;
-    colB.fv = d == J.x.ones ? 1.f : 0.f;
-    colB.voff = 8 * hh * ld4 + (colB.fill ? 0 : d) * 4;
-  }
-  const bool fillA = useA && ca + 31 >= J.x.cols, fillB = useB && cb + 31 >= J.x.cols;
-  const int wa = s3_half(32 * wave + cl, hh), wb = MT * 32 + wa;  // write offsets in a part
-  StageCursor lc;
-  lc.init(J, s0);
-  int cseg = lc.seg;
-  auto rsrc = [&](int seg) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(seg_base(J, segs, seg)), 0,
-                                             (int)(rows * ld4), 0x00020000);
-  };
-  __amdgpu_buffer_rsrc_t rs = rsrc(cseg);
-  float ra[8], rb[8];
-  int64_t rk = 0;  // first row (within its batch) of the loaded substep
-  auto load = [&](int hs) {
-    if (lc.seg != cseg) {
-      cseg = lc.seg;
-      rs = rsrc(cseg);
-    }
-    rk = lc.k + 16 * (hs & 1);
-    const int sb = (int)rk * ld4;
-    if (useA) x3_load8(ra, rs, colA, sb, ld4);
-    if (useB) x3_load8(rb, rs, colB, sb, ld4);
-    if (hs & 1) lc.next(rows);
-  };
-  auto put = [&](char* slot, int off, const float (&raw)[8], const X3Col& c, bool fill, int64_t k) {
-    float x[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) x[r] = raw[r];
-    if (fill && c.fill) {  // columns past the data: their fill (rows past the batch: 0)
-#pragma unroll
-      for (int r = 0; r < 8; ++r) x[r] = k + 8 * hh + r < rows ? c.fv : 0.f;
-    }
-    const X3Frag f = x3_split8(x);
-#pragma unroll
-    for (int p = 0; p < 3; ++p) *reinterpret_cast<bf16x8*>(slot + p * S3_PART + off) = f.p[p];
-  };
-  auto produce = [&](int hs, int64_t k) {
-    char* slot = lds + (hs % X3M_NSLOT) * S3_REG;
-    if (useA) put(slot, wa, ra, colA, fillA, k);
-    if (useB) put(slot, wb, rb, colB, fillB, k);
-  };
-  const int nh = 2 * ns;
-  if (nh > 0) {
-    load(0);
-    produce(0, rk);
-    if (nh > 1) load(1);
-    for (int hs = 0; hs < nh; ++hs) {
-      stage_barrier();  // slot hs written by every wave; the slot of hs - 1 is free
-      if (hs + 1 < nh) {
-        produce(hs + 1, rk);
-        if (hs + 2 < nh) load(hs + 2);
-      }
-      if (any) s3_consume_sub(lds + (hs % X3M_NSLOT) * S3_REG, oa, ob, act, acc);
-    }
-  }
-  const int ti = 2 * I + wr, tj = 2 * Jc + wc;
-  float* o = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.splits + split) * TILE * TILE;
-#pragma unroll
-  for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj)
-      if (act[bi][bj])
-        put_partial(J, acc[bi][bj],
-                    [&](int v) { return &o[(bi * 32 + acc_row(v, lane)) * TILE + bj * 32 + (lane & 31)]; });
-}
-
-__global__ __launch_bounds__(NTHREADS, 2) void kfac_factor_x3m(FactorArgs args) {
-  __shared__ __attribute__((aligned(16))) char lds[X3M_LDS];
-  const int task = xcd_task(blockIdx.x, gridDim.x);
-  int j = 0;
-  while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
-  const FactorJobDev& J = args.job[j];
-  const int local = task - J.task_begin;
-  if (J.n <= 32)
-    factor_task_narrow_direct(J, args.segs, local, reinterpret_cast<float*>(lds));
-  else
-    x3m_task(J, args.segs, local, lds);
-}
-#endif
-
 // Every job of the launch is LDS-DMA-eligible or narrow (n <= 32: direct loads).
-#ifndef KFAC_X3_OCC
-#define KFAC_X3_OCC (KFAC_X3_DIRECT ? 2 : 3)  // waves per SIMD the registers are sized for
-#endif
-__global__ __launch_bounds__(X3_THREADS, KFAC_X3_OCC) void kfac_factor_tiles_x3(FactorArgs args) {
-  // (direct loads: LDS only for the epilogue's hand-off of a block row, 16 KB)
-  __shared__ __attribute__((aligned(16))) float lds[(KFAC_X3_DIRECT ? 1 : 2) * 2 * BK * TILE];
+// 2 waves per SIMD (178 VGPRs): 4 workgroups per CU leave a 32-tile inversion
+// workgroup (107 registers, 29 KB) room to run beside the pass
+__global__ __launch_bounds__(X3_THREADS, 2) void kfac_factor_tiles_x3(FactorArgs args) {
+  // (LDS only for the epilogue's hand-off of a block row, 16 KB)
+  __shared__ __attribute__((aligned(16))) float lds[2 * BK * TILE];
   for (int i = 0; i < args.stagger * (int)(blockIdx.x >> 8); ++i) __builtin_amdgcn_s_sleep(8);
   const int task = xcd_task(blockIdx.x, gridDim.x);
   int j = 0;
@@ -1990,16 +1691,6 @@ static int tiles_x3_mode() {
   return m;
 }
 
-// kfac_factor_x3m (128 x 128 macro tiles, split in the kernel) instead of x3 for the
-// groups x3 takes: KFAC_X3M=1 (A/B knob).
-static bool x3m_on() {
-  static const bool on = [] {
-    const char* v = getenv("KFAC_X3M");
-    return v && v[0] == '1';
-  }();
-  return on;
-}
-
 static bool tiles_x3_group(const kfac_factor_job* jobs, int njobs) {
   if (tiles_x3_mode() == 0 || njobs <= 0 || syrk3_group(jobs, njobs)) return false;
   int nmax = 0;
@@ -2019,12 +1710,7 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
   const bool s3 = syrk3_group(jobs, njobs);
   // resident workgroups per CU: 4 (32 KB of LDS each); the bf16x3 kernel: S3D_WGS
   // (49 KB each)
-  const bool x3m = tiles_x3_group(jobs, njobs) && x3m_on();
-  static const int x3_wgs = [] {
-    const char* v = getenv("KFAC_X3_WGS");  // (A/B knob: resident x3 workgroups per CU planned for)
-    return v ? std::max(1, atoi(v)) : 4;
-  }();
-  if (slots <= 0) slots = (s3 ? S3D_WGS : x3m ? 2 : tiles_x3_group(jobs, njobs) ? x3_wgs : 4) * 256;
+  if (slots <= 0) slots = (s3 ? S3D_WGS : 4) * 256;
   constexpr int64_t MIN_CHUNK = 8, OVERHEAD = 4;  // stages; ~per-task fixed cost in stages
   int64_t max_steps = 1;
   for (int i = 0; i < njobs; ++i) max_steps = std::max(max_steps, job_stages(jobs[i]));
@@ -2033,7 +1719,7 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
     const int64_t t = cdiv(factor_n(jobs[i]), TILE);
     const int64_t t3 = cdiv(factor_n(jobs[i]), MT);
     ConvGeom cg;
-    if (s3 || x3m) units[i] = factor_n(jobs[i]) <= 32 ? 1 : t3 * (t3 + 1) / 2;
+    if (s3) units[i] = factor_n(jobs[i]) <= 32 ? 1 : t3 * (t3 + 1) / 2;
     else units[i] = conv_geom(jobs[i], cg) ? cg.units : t * (t + 1) / 2;
   }
   // workgroups of job i at `splits` K-splits
@@ -2262,9 +1948,7 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
               KFAC_CHECK_LAUNCH();
             }
             hipLaunchKernelGGL(kfac_factor_syrk3, dim3(tasks), dim3(NTHREADS), S3D_LDS, stream, args);
-          } else if (x3 && x3m_on())
-            hipLaunchKernelGGL(kfac_factor_x3m, dim3(tasks), dim3(NTHREADS), 0, stream, args);
-          else if (x3)
+          } else if (x3)
             hipLaunchKernelGGL(kfac_factor_tiles_x3, dim3(tasks), dim3(X3_THREADS), 0, stream, args);
           else if (all_glds)
             hipLaunchKernelGGL(kfac_factor_tiles_glds, dim3(tasks), dim3(NTHREADS), 0, stream, args);

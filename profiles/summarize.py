@@ -22,6 +22,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FETCH_X3_SCALE = 2.0  # FETCH_SIZE -> bytes for kfac_factor_tiles_x3's loads (see fetch_calib)
 
 
 def short(name):
@@ -48,19 +49,28 @@ def main(tag):
         stats[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3}
     with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
         json.dump(pmc, f, indent=1, sort_keys=True)
-    # the dominant factor kernel of the run: the bf16x3 SYRK when it ran (wide), else
-    # the fp32-MFMA one
-    kname = "kfac_factor_syrk3" if "FETCH_SIZE" in pmc.get("kfac_factor_syrk3", {}) else "kfac_factor_tiles"
+    # the dominant factor kernel of the run (most trace time): the fp32-MFMA SYRK, the
+    # split-pass bf16x3 SYRK (wide) or the register-split one (MNIST MLP)
+    cands = [k for k in ("kfac_factor_tiles", "kfac_factor_syrk3", "kfac_factor_tiles_x3")
+             if "FETCH_SIZE" in pmc.get(k, {}) and k in stats]
+    kname = max(cands, key=lambda k: stats[k]["calls"] * stats[k]["avg_us"]) if cands else "kfac_factor_tiles"
     t = pmc.get(kname, {})
     if "FETCH_SIZE" in t and "WRITE_SIZE" in t:
-        fetch = t["FETCH_SIZE"]["mean_per_dispatch"] * 1024 * 2  # gfx950: x2 for 16 B/lane reads
+        # FETCH_SIZE scale: x2 for 16 B/lane reads (MI355X_MICROARCH.md); the x3 kernel's
+        # 4 B/lane buffer loads are calibrated by tools/fetch_calib.py (FETCH_X3_SCALE)
+        scale = FETCH_X3_SCALE if kname == "kfac_factor_tiles_x3" else 2.0
+        fetch = t["FETCH_SIZE"]["mean_per_dispatch"] * 1024 * scale
         write = t["WRITE_SIZE"]["mean_per_dispatch"] * 1024
-        note = ("FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->bytes, "
+        note = (f"FETCH_SIZE x{scale:g} (gfx950 read-width correction) + WRITE_SIZE, KiB->bytes, "
                 "mean over the bench's launches (15 updates per pass, last batch short)")
         if kname == "kfac_factor_syrk3":
             note += ("; kfac_factor_syrk3 reads the split pass's bf16x3 panel images "
                      "(6 B per operand element) by global_load_lds_dwordx4 (16 B/lane: the x2 "
                      "applies); the split pass (kfac_split3) is a separate launch")
+        if kname == "kfac_factor_tiles_x3":
+            note += ("; kfac_factor_tiles_x3 reads fp32 operand rows by buffer_load_dword "
+                     "(4 B/lane, 128 B per half-wave): scale calibrated on a 512 MB operand "
+                     "read once (profiles/r03_x3/fetch_calib.txt)")
         out = {"kernel": kname, "tag": tag, "fetch_bytes_per_launch": fetch,
                "write_bytes_per_launch": write, "hbm_bytes_per_launch": fetch + write,
                "rocprof_trace": stats.get(kname), "note": note}
