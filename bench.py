@@ -370,12 +370,20 @@ def main(argv=None):
             comm.setdefault("events", []).append((e0, e1))
         kfac.allreduce = timed_allreduce
 
+    # the batches' record views, made once: in training the hooks hand KFAC fresh
+    # tensors per batch at no cost of its own, so slicing the resident records
+    # (~2.7 us of host time per view, 60 per MLP pass) stays out of the timed loop
+    views = [[(layer, [a[i:i + batch], g[i:i + batch]]) for layer, (a, g) in zip(layers, recs)]
+             for i in starts]
+    sizes = [min(batch, images - i) for i in starts]
+    record = kfac.record
+
     def one_pass():
         kfac.reset()
-        for i in starts:
-            for layer, (a, g) in zip(layers, recs):
-                kfac.record[layer] = [a[i:i + batch], g[i:i + batch]]
-            kfac.update(batch_size=min(batch, images - i))
+        for batch_views, size in zip(views, sizes):
+            for layer, rec in batch_views:
+                record[layer] = rec
+            kfac.update(batch_size=size)
         kfac.invert(*DAMPING)
 
     def sync():
@@ -491,6 +499,8 @@ def main(argv=None):
 
         def e2e_pass():
             kfac.reset()
+            for layer in layers:  # own record lists (the hooks fill them in place)
+                record[layer] = [None, None]
             for i in starts:
                 logits = net(x[i:i + batch])
                 labels = torch.distributions.Categorical(logits=logits).sample()

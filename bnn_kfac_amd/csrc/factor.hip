@@ -504,7 +504,10 @@ __device__ __forceinline__ float sub_f32(float x, float y) {
   return r;
 }
 
-// (a, b) -> their hi / mid / lo bf16 parts, packed as pairs (a low, b high)
+// (a, b) -> their hi / mid / lo bf16 parts, packed as pairs (a low, b high).
+// (x - part as one v_dot2c_f32_bf16, x + part * (-1) + 0 * other half, would save the
+// expansion of each part: tried, but the instruction's result is not exact -- factor
+// parity failed at 1.5e-4 relative -- so the residuals stay v_sub_f32.)
 __device__ __forceinline__ void split3(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
   h = bf16_pair(a, b);
   const float ra = sub_f32(a, __uint_as_float(h << 16)), rb = sub_f32(b, __uint_as_float(h & 0xffff0000u));
@@ -1709,8 +1712,12 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
                       int64_t slots = 0) {
   const bool s3 = syrk3_group(jobs, njobs);
   // resident workgroups per CU: 4 (32 KB of LDS each); the bf16x3 kernel: S3D_WGS
-  // (49 KB each)
-  if (slots <= 0) slots = (s3 ? S3D_WGS : 4) * 256;
+  // (49 KB each); kfac_factor_tiles_x3: KFAC_X3_WGS (A/B knob, default 4)
+  static const int x3_wgs = [] {
+    const char* v = getenv("KFAC_X3_WGS");
+    return v && atoi(v) > 0 ? atoi(v) : 4;
+  }();
+  if (slots <= 0) slots = (s3 ? S3D_WGS : tiles_x3_group(jobs, njobs) ? x3_wgs : 4) * 256;
   constexpr int64_t MIN_CHUNK = 8, OVERHEAD = 4;  // stages; ~per-task fixed cost in stages
   int64_t max_steps = 1;
   for (int i = 0; i < njobs; ++i) max_steps = std::max(max_steps, job_stages(jobs[i]));

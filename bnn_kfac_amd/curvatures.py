@@ -447,8 +447,13 @@ class KFAC(Curvature):
             forward, backward = self.record[layer]
             if kept[0] is not forward or kept[1] is not backward:
                 return  # a reshaped / made-contiguous record: stay on the slow path
+            if forward.dtype != backward.dtype or forward.device != backward.device:
+                return
             lst = self._state[layer]
-            spec.append((layer, self._signature(forward), self._signature(backward), lst, lst[0], lst[1]))
+            # (shapes, strides, dtype, device index: _fast_entry compares them field by
+            # field, cheapest first; the signature of _signature, unpacked)
+            spec.append((layer, forward.shape, backward.shape, forward.stride(), backward.stride(),
+                         forward.dtype, forward.get_device(), lst, lst[0], lst[1]))
         tmpl = []
         for j in jobs:
             t = N.FactorJob.from_buffer_copy(j)
@@ -463,19 +468,22 @@ class KFAC(Curvature):
         scale, spec, tmpl, device = self._fast
         if getattr(self, "_scale", 1.0) != scale:
             return None
-        record, state, sig = self.record, self._state, self._signature
-        ptrs, keep = [], []
-        for layer, sig_f, sig_b, lst, A, G in spec:
+        record, state = self.record, self._state
+        ptrs, keep, versions = [], [], []
+        for layer, shp_f, shp_b, str_f, str_b, dtype, dev, lst, A, G in spec:
             forward, backward = record[layer]
-            if forward is None or backward is None or sig(forward) != sig_f or sig(backward) != sig_b:
+            if forward is None or backward is None:
+                return None
+            if (forward.shape != shp_f or backward.shape != shp_b or forward.dtype != dtype
+                    or backward.dtype != dtype or forward.stride() != str_f or backward.stride() != str_b
+                    or forward.get_device() != dev or backward.get_device() != dev):
                 return None
             if state.get(layer) is not lst or lst[0] is not A or lst[1] is not G:
                 return None
-            ptrs.append(forward.data_ptr())
-            ptrs.append(backward.data_ptr())
-            keep.append(forward)
-            keep.append(backward)
-        return tmpl, tuple(ptrs), keep, [t._version for t in keep], device, tmpl
+            ptrs += (forward.data_ptr(), backward.data_ptr())
+            keep += (forward, backward)
+            versions += (forward._version, backward._version)
+        return tmpl, tuple(ptrs), keep, versions, device, tmpl
 
     def _enqueue(self, entry):
         """Queue one update: (jobs, operand pointers, records kept alive, their
