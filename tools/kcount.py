@@ -21,8 +21,9 @@ def main(path, pat):
         print(name, sum(c.values()))
         print("  ", ", ".join("%s %d" % kv for kv in c.most_common(18)))
         i = meta.find(".name:           " + name)
-        blk = meta[meta.rfind("- .a", 0, i):i] if i >= 0 else ""
-        print("  ", re.findall(r"\.(vgpr_count|sgpr_count|vgpr_spill_count):\s+(\d+)", blk))
+        j = meta.find("\n  - ", i) if i >= 0 else -1
+        blk = meta[meta.rfind("\n  - ", 0, i):j if j > 0 else len(meta)] if i >= 0 else ""
+        print("  ", re.findall(r"\.(vgpr_count|agpr_count|sgpr_count|vgpr_spill_count|group_segment_fixed_size):\s+(\d+)", blk))
 
 
 if __name__ == "__main__":
