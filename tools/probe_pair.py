@@ -1,8 +1,9 @@
 """Time the MLP's grouped inversion (785, 128, 129, 10 factors, invert(0.04, 200)) alone
-on the GPU: HIP-event time per call, mean of `reps`.  For the A/B of the paired-step
-chain (KFAC_INV_PAIR) and the tasks-per-workgroup knob (KFAC_INV_TPW).  GPU only.
+on the GPU: HIP-event time per call, mean of `reps`.  Written for the A/B of the
+paired-step chain (commit d327996, KFAC_INV_PAIR, removed after it) and the
+tasks-per-workgroup knob (KFAC_INV_TPW).  GPU only.
 
-    KFAC_INV_PAIR=1 python tools/probe_pair.py [reps]
+    python tools/probe_pair.py [reps]
 """
 import os
 import sys
