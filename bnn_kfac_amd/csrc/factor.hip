@@ -1353,18 +1353,20 @@ __global__ __launch_bounds__(NTHREADS) void kfac_factor_channel_small(FactorArgs
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = op.cols;
   const int64_t b0 = (int64_t)split * cg.B / J.splits, b1 = (int64_t)(split + 1) * cg.B / J.splits;
-  const int64_t L4 = op.L >> 2, per = (b1 - b0) * L4;  // (image, 4-position run) pairs
+  // (image, 4-position run) pairs of the task: 32-bit index math (a task's pairs and a
+  // job's images fit 32 bits; the 64-bit divisions cost as much issue as the FMAs)
+  const uint32_t L4 = (uint32_t)(op.L >> 2), per = (uint32_t)(b1 - b0) * L4;
   float acc[NT];
 #pragma unroll
   for (int e = 0; e < NT; ++e) acc[e] = 0.f;
   // two (image, run) pairs per trip, their 2 x n float4 loads issued together
-  auto src_of = [&](int64_t q) {
-    const int64_t img = q / L4, r4 = q - img * L4;
+  auto src_of = [&](uint32_t q) {
+    const uint32_t img = q / L4, r4 = q - img * L4;
     // image b0 + img of the job: batch seg of the queued batches, image bi in it
-    const uint32_t ab = (uint32_t)(b0 + img), seg = ab / (uint32_t)cg.bseg;
+    const uint32_t ab = (uint32_t)b0 + img, seg = ab / (uint32_t)cg.bseg;
     return seg_base(J, args.segs, (int)seg) + (int64_t)(ab - seg * cg.bseg) * op.sB + 4 * r4;
   };
-  for (int64_t q = tid; q < per; q += 2 * NTHREADS) {
+  for (uint32_t q = tid; q < per; q += 2 * NTHREADS) {
     const bool two = q + NTHREADS < per;
     const float* s0 = src_of(q);
     const float* s1 = two ? src_of(q + NTHREADS) : s0;
