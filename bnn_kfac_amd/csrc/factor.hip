@@ -1013,12 +1013,7 @@ struct ConvGeom {
 #ifndef KFAC_CONV_OCC
 #define KFAC_CONV_OCC 4  // resident workgroups per CU the mode-0 instances are compiled for
 #endif
-// X3 (mode 0 only): the blocks' products as bf16x3 MFMAs (v_mfma_f32_32x32x16_bf16,
-// six per fp32 product, the split of kfac_factor_tiles_x3 made in registers): a
-// lane's 8 k-values are 8 consecutive positions t0 .. t0+7 of its row group / segment
-// (one LDS read each, the A value masked past the row's end), so one set of six MFMAs
-// covers the 2 x 8 positions eight 32x32x2 fp32 MFMAs did
-template <int LAYOUT, int PMAXE, bool STRIDE1, int CB = CONV_CB, bool M3 = false, bool X3 = false>
+template <int LAYOUT, int PMAXE, bool STRIDE1, int CB = CONV_CB, bool M3 = false>
 __global__ __launch_bounds__(NTHREADS, (CB == 2 && !M3) ? KFAC_CONV_OCC : 4) void kfac_factor_conv(
     FactorArgs args, ConvGeom cg) {
   extern __shared__ __attribute__((aligned(16))) float cimg[];
@@ -1225,42 +1220,9 @@ __global__ __launch_bounds__(NTHREADS, (CB == 2 && !M3) ? KFAC_CONV_OCC : 4) voi
       }
     }
   };
-  // X3: one row group of one block, 8 positions per step; a diagonal block (same
-  // columns, and rows past Ho read A from the zero plane) splits its A fragment once
-  auto row_x3 = [&](const float* pa, const float* pb, bool same_ab, floatx16& a) {
-    const int st = STRIDE1 ? 1 : cg.stride, T = cg.T, last = (T - 1) * st;
-    for (int t0 = 0; t0 < T; t0 += 8) {
-      float xa[8], xb[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int o = min((t0 + u) * st, last);
-        xa[u] = pa[o];
-        if (!same_ab) xb[u] = pb[o];
-      }
-      if (t0 + 8 > T) {  // (wave-uniform) positions past the row: A = 0
-#pragma unroll
-        for (int u = 0; u < 8; ++u) xa[u] = t0 + u < T ? xa[u] : 0.f;
-      }
-      const X3Frag fa = x3_split8(xa);
-      if (same_ab) {
-        x3_six(a, fa, fa);
-      } else {
-        const X3Frag fb = x3_split8(xb);
-        x3_six(a, fa, fb);
-      }
-    }
-  };
   // one row group of every block of this wave (rowA / rowB: LDS offsets added to the
   // blocks' column offsets; zeroA: A read from the zero plane)
   auto blocks = [&](int rowA, int rowB, bool zeroA) {
-    if constexpr (X3) {
-#pragma unroll
-      for (int i = 0; i < CB; ++i) {
-        if (i >= nmine) break;
-        row_x3(cimg + (zeroA ? cg.zero_base : offA[i] + rowA), cimg + offB[i] + rowB, same[i], acc[i]);
-      }
-      return;
-    }
     if constexpr (M3) {  // both operands from the same reads: a row past Ho reads zeros
       row_mfmas3(cimg + (zeroA ? cg.zero_base : offA[0] + rowA),
                  cimg + (zeroA ? cg.zero_base : offA[CB - 1] + rowA));
@@ -1539,15 +1501,6 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
   return true;
 }
 
-// bf16x3 products for the staged conv kernel's mode 0 (KFAC_CONV_X3=1 / 0)
-static int conv_x3_mode() {
-  static const int m = [] {
-    const char* v = getenv("KFAC_CONV_X3");
-    return v && v[0] == '1' ? 1 : 0;
-  }();
-  return m;
-}
-
 template <int LAYOUT>
 static void launch_conv(const FactorArgs& args, const ConvGeom& g, int tasks, hipStream_t stream) {
   if (LAYOUT == KFAC_CHANNEL && g.n <= 8 && !conv_small_off()) {
@@ -1563,19 +1516,12 @@ static void launch_conv(const FactorArgs& args, const ConvGeom& g, int tasks, hi
   }
   const size_t shmem = (size_t)g.lds * sizeof(float);
   const bool s1 = g.stride == 1;
-  const bool x3 = g.mode == 0 && conv_x3_mode() == 1;
   const int pm = (int)cdiv(g.src, NTHREADS);  // <= 8 by CONV_SRC_MAX
   // one instance per mode class, so each gets its own register budget: mode 0 (CB
   // blocks per wave), the one-block narrow modes 1 / 2 (CB = 1), mode 3
-#define KFAC_CONV_LAUNCH(PM, S1, CBV, M3)                                                                   \
-  do {                                                                                                      \
-    if (x3)                                                                                                 \
-      hipLaunchKernelGGL((kfac_factor_conv<LAYOUT, PM, S1, CBV, M3, true>), dim3(tasks), dim3(NTHREADS), shmem, \
-                         stream, args, g);                                                                  \
-    else                                                                                                    \
-      hipLaunchKernelGGL((kfac_factor_conv<LAYOUT, PM, S1, CBV, M3>), dim3(tasks), dim3(NTHREADS), shmem,    \
-                         stream, args, g);                                                                  \
-  } while (0)
+#define KFAC_CONV_LAUNCH(PM, S1, CBV, M3) \
+  hipLaunchKernelGGL((kfac_factor_conv<LAYOUT, PM, S1, CBV, M3>), dim3(tasks), dim3(NTHREADS), shmem, stream, \
+                     args, g)
 #define KFAC_CONV_PICK(CBV, M3)                                                   \
   do {                                                                            \
     if (pm <= 4) {                                                                \
