@@ -1470,8 +1470,12 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
     g.T = o.Wo;
     g.G = (int)cdiv(o.Ho, g.KR);
     g.stride = o.sw;
-    g.ones_base = o.C * g.plane;
+    g.ones_base = o.C * g.plane;  // (= n - 1 mod 32: the bias column's own bank)
+    // the padding columns of the last block all read the zero plane (one broadcast
+    // address): put it on bank n mod 32, which no data column of that block uses
+    // (at its unpadded place it shared a bank with one: 2-way conflicts)
     g.zero_base = g.ones_base + o.Ho * g.rowstep;
+    g.zero_base += (int)((((int64_t)n - g.zero_base) % 32 + 32) % 32);
     lds = (int64_t)g.zero_base + o.Ho * g.rowstep;
     g.src = o.C * o.H * o.W;
   } else {
