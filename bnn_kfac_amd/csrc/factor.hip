@@ -1717,13 +1717,9 @@ static bool tiles_x3_group(const kfac_factor_job* jobs, int njobs) {
 static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
                       int64_t slots = 0) {
   const bool s3 = syrk3_group(jobs, njobs);
-  // resident workgroups per CU: 4 (32 KB of LDS each); the bf16x3 kernel: S3D_WGS
-  // (49 KB each); kfac_factor_tiles_x3: KFAC_X3_WGS (A/B knob, default 4)
-  static const int x3_wgs = [] {
-    const char* v = getenv("KFAC_X3_WGS");
-    return v && atoi(v) > 0 ? atoi(v) : 4;
-  }();
-  if (slots <= 0) slots = (s3 ? S3D_WGS : tiles_x3_group(jobs, njobs) ? x3_wgs : 4) * 256;
+  // resident workgroups per CU: 4 (32 KB of LDS each; kfac_factor_tiles_x3: 4 of two
+  // waves -- 3 or 2 measured slower); the bf16x3 kernel: S3D_WGS (49 KB each)
+  if (slots <= 0) slots = (s3 ? S3D_WGS : 4) * 256;
   constexpr int64_t MIN_CHUNK = 8, OVERHEAD = 4;  // stages; ~per-task fixed cost in stages
   int64_t max_steps = 1;
   for (int i = 0; i < njobs; ++i) max_steps = std::max(max_steps, job_stages(jobs[i]));
