@@ -298,7 +298,8 @@ def main(argv=None):
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-serial", action="store_true")
     ap.add_argument("--launch-first", type=int, default=None,
-                    help="queued updates in a pass's first SYRK launch (KFAC.launch_first)")
+                    help="queued updates in a pass's first SYRK launch (KFAC.launch_first) for both "
+                         "loops (default: 16 for the pipelined loop, the library's 1 for the serial one)")
     ap.add_argument("--single-buffer", action="store_true",
                     help="KFAC.double_buffer = False (the data stream waits for each "
                          "inversion to have read its factors)")
@@ -346,8 +347,15 @@ def main(argv=None):
     # the reference's behaviour), so pass k+1 is queued behind inversion k and
     # overlaps it; every verdict is still read inside the timed region below
     kfac.eager_verdict = False
-    if args.launch_first:
-        kfac.launch_first = args.launch_first
+    # pipelined loop: the pass's queued updates go out as ONE SYRK launch at the flush
+    # (launch_first 16 >= the MLP's 15 updates; the records-held cap splits LeNet-5's
+    # passes anyway): the inversion of pass k overlaps the host's issue of pass k+1
+    # as well as its SYRK.  MLP line, one box, 2 reps: 1.51-1.53e8 vs 1.41e8 img/s at
+    # the library default 1; the serial loop keeps 1 (8.6e7 vs 8.0e7 img/s at 16:
+    # there the GPU would wait for the host to queue the pass) -- profiles/r03_knobs/
+    pipe_launch_first = args.launch_first or 16
+    serial_launch_first = args.launch_first or kfac.launch_first
+    kfac.launch_first = pipe_launch_first
     if args.single_buffer:
         kfac.double_buffer = False
     recs = synthetic_records(specs, images, device, seed=1234 + rank)
@@ -480,6 +488,7 @@ def main(argv=None):
         # the caller who runs a pass, inverts on its own stream and reads the result
         # before the next pass (classification_ll_block.py:93-106): no overlap
         kfac.overlap_invert = False
+        kfac.launch_first = serial_launch_first
         one_pass()
         kfac.inv_state
         sync()
@@ -491,6 +500,7 @@ def main(argv=None):
         sync()
         serial = world * images * args.steps / max_over_ranks(time.perf_counter() - t1)
         kfac.overlap_invert = True
+        kfac.launch_first = pipe_launch_first
 
     e2e = None
     if not args.no_e2e and world == 1:
@@ -552,7 +562,8 @@ def main(argv=None):
                           "global_batch": batch * world,
                           "images_per_rank": images, "parallelism": f"dp{world}",
                           "inversion": ("sharded" if getattr(kfac, "_sharded_last", False)
-                                        else "replicated")},
+                                        else "replicated"),
+                          "launch_first": {"pipelined": pipe_launch_first, "serial": serial_launch_first}},
                "roofline": roofline, "cpu_baseline": cpu, "breakdown": breakdown,
                "allreduce_ms_per_step": allreduce_ms,
                "serial_images_per_s": serial, "e2e_images_per_s": e2e}
