@@ -208,7 +208,10 @@ class KFAC(Curvature):
         # queued updates keep their records alive until their launch (the reference
         # frees them after each update): the queue is also launched once the records
         # it holds reach this many bytes, so a wide or conv model's activations are
-        # not retained beyond ~this much (MLP batch of 4096: 17 MB per update)
+        # not retained beyond ~this much (MLP batch of 4096: 17 MB per update; LeNet-5
+        # batch of 1024: ~35 MB; the wide MLP: 281 MB, one update per launch).  1 GiB
+        # measured +6.6 % on LeNet-5 but -8 % on the wide MLP (3-update split-pass
+        # launches): 256 MiB stays
         self.defer_bytes = 256 << 20
         self._queue_bytes = 0
         self._queue = []         # per queued update: (jobs, operand pointers, kept records,
