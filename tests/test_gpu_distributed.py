@@ -49,7 +49,7 @@ def _net(dev):
                                torch.nn.Linear(128, 10)).to(dev)
 
 
-def _worker(rank, world, port, q, shape, shard, backend):
+def _worker(rank, world, port, q, shape, shard, backend, launch_first=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     dev = torch.device("cuda:0")
@@ -63,6 +63,7 @@ def _worker(rank, world, port, q, shape, shard, backend):
         net = _net(dev)
         kfac = DistributedKFAC(net, shard_inversion=shard)
         kfac.always_reduce = True
+        kfac.launch_first = launch_first  # (16: the bench's pipelined loop, a pass per launch)
         for p in range(SIZES[shape][1]):
             kfac.reset()
             for a1, g1, a2, g2 in _data(shape):
@@ -94,11 +95,11 @@ def _single_device(dev, shape):
             [t.cpu().numpy() for pair in kfac.inv_state.values() for t in pair])
 
 
-def _run(world, shape, shard, backend="gloo"):
+def _run(world, shape, shard, backend="gloo", launch_first=1):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, shape, shard, backend))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, shape, shard, backend, launch_first))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -124,9 +125,10 @@ def _check(results, want_st, want_inv, shard):
         np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("shape,shard", [("small", False), ("c4", False), ("small", True)])
-def test_two_ranks_match_single_device(hip_device, shape, shard):
-    results = _run(2, shape, shard)
+@pytest.mark.parametrize("shape,shard,lf", [("small", False, 1), ("c4", False, 1), ("small", True, 1),
+                                            ("c4", False, 16)])
+def test_two_ranks_match_single_device(hip_device, shape, shard, lf):
+    results = _run(2, shape, shard, launch_first=lf)
     want_st, want_inv = _single_device(hip_device, shape)
     _check(results, want_st, want_inv, shard)
 
