@@ -159,6 +159,26 @@ def cpu_model():
     return None
 
 
+def host_cpus():
+    """What this process may run on: its CPU affinity, the cgroup CPU quota (cpu.max,
+    None when unlimited) and OMP_NUM_THREADS."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0")) or None
+    return {"affinity": affinity, "cgroup_quota_cpus": quota, "omp_num_threads": omp,
+            "logical_cpus": os.cpu_count()}
+
+
 def cpu_baseline(layers, images, batch, budget_s=12.0, threads=None):
     """The reference's CPU op sequence (oracle/cpu_ref_torch.py) on the same workload,
     bounded to ~budget_s seconds of batches (whole passes when they fit; else the
@@ -216,6 +236,86 @@ def cpu_e2e_baseline(config, images, batch, budget_s=6.0, threads=None):
     return done / dt, threads, (f"{done} synthetic images, batch {batch}: forward + Categorical labels + "
                                 f"CE backward + update (reference hooks) + invert per group of batches, "
                                 f"torch {torch.__version__} CPU fp32, {threads} thread(s)")
+
+
+def verify_parity(kfac, net, specs, recs, batch, images, world, rank, device, sync, nbatches=2,
+                  seed0=1234, ref_factory=None):
+    """N > 1 self-check, run after the timed region: is the sharded pass + all-reduce
+    the single-device pass of the same global batches (models/curvatures.py:359-363)?
+
+    * every rank runs `nbatches` of its batches through the data-parallel `kfac`
+      (alpha = 1 / global batch, ONE all-reduce of the packed triangles, invert);
+    * rank 0 regenerates every rank's records (same seeds: synthetic_records is a
+      function of (seed, shape) only; a per-rank float64 checksum of the rows used
+      guards that), concatenates each global batch in rank order and runs a plain
+      single-device KFAC over them;
+    * rank 0 compares the reduced factors at rtol 1e-5 (of each factor's max) and the
+      L factors at 1e-4 of max|L| (the north-star tolerance; the reduced factors
+      differ from the single-device sums in the last bits, which cond(R) amplifies);
+    * every rank checks that it holds bit-identical L factors (rank 0's broadcast).
+    Returns {"ok": bool, ...} on every rank (the verdict is broadcast)."""
+    from bnn_kfac_amd.curvatures import KFAC
+    layers = [m for m in net.modules() if isinstance(m, (torch.nn.Linear, torch.nn.Conv2d))]
+    rows = [min(batch, images - i) for i in range(0, images, batch)][:nbatches]
+    starts = [sum(rows[:b]) for b in range(len(rows))]
+    kfac.reset()
+    for s, n in zip(starts, rows):
+        for layer, (a, g) in zip(layers, recs):
+            kfac.record[layer] = [a[s:s + n], g[s:s + n]]
+        kfac.update(batch_size=n, global_batch_size=n * world)
+    kfac.invert(*DAMPING)
+    inv = kfac.inv_state
+    mine_F = [F_ for layer in layers for F_ in kfac.state[layer]]
+    mine_L = [L_ for layer in layers for L_ in inv[layer]]
+    sync()
+    used = sum(rows)
+    csum = torch.tensor([float(sum(t[:used].double().sum() for pair in recs for t in pair))],
+                        dtype=torch.float64, device=device)
+    sums = [torch.zeros_like(csum) for _ in range(world)]
+    dist.all_gather(sums, csum)
+    detail = {"batches": len(rows), "global_batch": batch * world, "rows_per_rank": used,
+              "tolerance": "factors rtol 1e-5 of max|F|; L atol 1e-4 of max|L|; L bit-identical on all ranks"}
+    verdict = torch.zeros(1, dtype=torch.float64, device=device)
+    if rank == 0:
+        per_rank = [recs]
+        ok_sums = True
+        for r in range(1, world):
+            other = synthetic_records(specs, images, device, seed=seed0 + r)
+            other = [(a[:used].clone(), g[:used].clone()) for a, g in other]
+            got = float(sum(t.double().sum() for pair in other for t in pair))
+            ok_sums &= abs(got - float(sums[r])) <= 1e-9 * max(1.0, abs(got))
+            per_rank.append(other)
+        ref = (ref_factory or KFAC)(net)
+        for s, n in zip(starts, rows):
+            for li, layer in enumerate(layers):
+                a = torch.cat([pr[li][0][s:s + n] for pr in per_rank])
+                g = torch.cat([pr[li][1][s:s + n] for pr in per_rank])
+                ref.record[layer] = [a, g]
+            ref.update(batch_size=n * world)
+        ref.invert(*DAMPING)
+        ref_inv = ref.inv_state
+        for h in ref.hooks:
+            h.remove()
+        want_F = [F_ for layer in layers for F_ in ref.state[layer]]
+        want_L = [L_ for layer in layers for L_ in ref_inv[layer]]
+        err_F = max(float((g - w).abs().max() / w.abs().max().clamp_min(1e-30)) for g, w in zip(mine_F, want_F))
+        err_L = max(float((g - w).abs().max() / w.abs().max().clamp_min(1e-30)) for g, w in zip(mine_L, want_L))
+        upper = all(bool((torch.triu(L_, 1) == 0).all()) for L_ in mine_L)
+        ok = ok_sums and err_F <= 1e-5 and err_L <= 1e-4 and upper
+        detail.update({"records_checksum_match": ok_sums, "max_rel_err_factors": err_F,
+                       "max_rel_err_L": err_L, "L_lower_triangular": upper})
+        verdict.fill_(1.0 if ok else 0.0)
+        del ref, per_rank
+    # every rank holds the same L factors, bit for bit
+    flat = torch.cat([L_.reshape(-1) for L_ in mine_L])
+    root = flat.clone()
+    dist.broadcast(root, 0)
+    same = torch.tensor([1.0 if torch.equal(root, flat) else 0.0], dtype=torch.float64, device=device)
+    dist.all_reduce(same, op=dist.ReduceOp.MIN)
+    dist.broadcast(verdict, 0)
+    detail["identical_L_all_ranks"] = bool(float(same) == 1.0)
+    detail["ok"] = bool(float(verdict) == 1.0) and detail["identical_L_all_ranks"]
+    return detail
 
 
 def load_traffic(config):
@@ -305,12 +405,17 @@ def main(argv=None):
     ap.add_argument("--single-buffer", action="store_true",
                     help="KFAC.double_buffer = False (the data stream waits for each "
                          "inversion to have read its factors)")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="N > 1: skip the post-timing verification pass (verify_parity)")
+    ap.add_argument("--shared-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank on device 0, gloo instead of RCCL "
+                         "(the line says so in config.parallelism; never a scaling number)")
     argv = sys.argv[1:] if argv is None else argv
     args = ap.parse_args(argv)
 
     if "WORLD_SIZE" not in os.environ:
         if args.gpus > 1:
-            return spawn_ranks(args.gpus, argv)
+            return spawn_ranks(args.gpus, argv, check_devices=not args.shared_device)
         world = 1
     else:
         world = int(os.environ["WORLD_SIZE"])
@@ -319,7 +424,7 @@ def main(argv=None):
                   file=sys.stderr, flush=True)
             return 2
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.shared_device else int(os.environ.get("LOCAL_RANK", "0"))
     if torch.cuda.device_count() <= local:
         print(f"bench.py rank {rank}: LOCAL_RANK {local} but only {torch.cuda.device_count()} GPU(s) "
               f"visible", file=sys.stderr, flush=True)
@@ -332,7 +437,10 @@ def main(argv=None):
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.shared_device:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
     # all GPU work on one non-default stream
     torch.cuda.set_stream(torch.cuda.Stream(device))
 
@@ -506,6 +614,10 @@ def main(argv=None):
         kfac.overlap_invert = True
         kfac.launch_first = pipe_launch_first
 
+    parity = None
+    if world > 1 and not args.no_parity:
+        parity = verify_parity(kfac, net, specs, recs, batch, images, world, rank, device, sync)
+
     e2e = None
     if not args.no_e2e and world == 1:
         x = torch.rand(images, *specs[0].in_shape, device=device)
@@ -536,16 +648,25 @@ def main(argv=None):
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        v, cores, sample = cpu_baseline(specs, images, batch)
+        # the host's best: every thread count this process may use -- its CPU affinity,
+        # its cgroup CPU quota and OMP_NUM_THREADS (the box's per-GPU share) -- timed,
+        # the fastest reported (`cores` = its thread count), and 1 thread beside them
+        hc = host_cpus()
+        quota = int(hc["cgroup_quota_cpus"]) if hc["cgroup_quota_cpus"] else None
+        counts = sorted({c for c in (hc["affinity"], hc["omp_num_threads"], quota) if c})
+        runs = {c: cpu_baseline(specs, images, batch, threads=c) for c in counts}
+        best = max(runs, key=lambda c: runs[c][0])
+        v, cores, sample = runs[best]
         v1, _, sample1 = cpu_baseline(specs, images, batch, budget_s=6.0, threads=1)
         cpu = {"value": v, "unit": "images/s", "cores": cores, "kind": "port", "sample": sample,
+               "value_by_threads": {str(c): r[0] for c, r in runs.items()},
                "value_1_thread": v1, "sample_1_thread": sample1, "cpu_model": cpu_model(),
-               "logical_cpus_visible": os.cpu_count()}
+               "host_cpus": hc, "logical_cpus_visible": os.cpu_count()}
         if args.config == "mlp":
             # BASELINE C1: the reference's CPU pass at ITS batch (256), and the CPU
             # end-to-end loop beside the GPU's e2e_images_per_s
-            vc1, _, samplec1 = cpu_baseline(specs, 60000, 256, budget_s=6.0)
-            ve, _, samplee = cpu_e2e_baseline(args.config, 60000, 256)
+            vc1, _, samplec1 = cpu_baseline(specs, 60000, 256, budget_s=6.0, threads=cores)
+            ve, _, samplee = cpu_e2e_baseline(args.config, 60000, 256, threads=cores)
             cpu.update({"c1_batch256_value": vc1, "c1_batch256_sample": samplec1,
                         "e2e_value": ve, "e2e_sample": samplee})
 
@@ -564,12 +685,17 @@ def main(argv=None):
                                       f"+ invert{DAMPING}",
                           "baseline_config": cfg + (" strong" if args.strong else ""),
                           "global_batch": batch * world,
-                          "images_per_rank": images, "parallelism": f"dp{world}",
+                          "images_per_rank": images,
+                          "parallelism": f"dp{world}" + (" (shared device, gloo: rehearsal, not a "
+                                                         "scaling number)" if args.shared_device else ""),
                           "inversion": ("sharded" if getattr(kfac, "_sharded_last", False)
                                         else "replicated"),
                           "launch_first": {"pipelined": pipe_launch_first, "serial": serial_launch_first}},
                "roofline": roofline, "cpu_baseline": cpu, "breakdown": breakdown,
                "allreduce_ms_per_step": allreduce_ms,
+               # N > 1: the sharded pass + all-reduce vs a single-device recompute of the
+               # same global batches (verify_parity, after the timed region); N = 1: null
+               "parity": None if parity is None else parity["ok"], "parity_detail": parity,
                "serial_images_per_s": serial, "e2e_images_per_s": e2e}
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -7,6 +7,7 @@ on the tensor's device, passed to every call explicitly.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import threading
@@ -124,6 +125,7 @@ SIGNATURES = {
     "kfac_profile_read": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_int64)]),
     "kfac_profile_reset": (ctypes.c_int, []),
+    "kfac_release": (ctypes.c_int, []),
     "kfac_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "kfac_version": (ctypes.c_char_p, []),
 }
@@ -152,7 +154,18 @@ def lib():
                     fn.restype = res
                     fn.argtypes = args
                 _lib = handle
+                # the library's cached hipGraphs / events go while the HIP runtime is
+                # still up (Python's atexit runs before the C runtime's exit handlers)
+                atexit.register(_release_at_exit)
     return _lib
+
+
+def _release_at_exit():
+    try:
+        if _lib is not None and torch.cuda.is_initialized():
+            _lib.kfac_release()
+    except Exception:  # exiting anyway: never mask the process's own status
+        pass
 
 
 def check(rc: int, what: str):

@@ -89,6 +89,32 @@ extern "C" int kfac_profile_read(int id, double* total_ms, int64_t* launches) {
   return KFAC_OK;
 }
 
+// Every HIP object the library keeps across calls -- the inversion's cached graphs,
+// their replay events, the profiling event pool -- released while the HIP runtime
+// is still up (the Python binding registers it with atexit).  Later calls rebuild
+// what they need, so it is also safe mid-process.
+int kfac_release_graphs();  // invert.hip
+
+extern "C" int kfac_release(void) {
+  int rc = kfac_release_graphs();
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_on = false;
+  for (const Rec& r : g_open) {
+    (void)hipEventDestroy(r.start);
+    (void)hipEventDestroy(r.stop);
+  }
+  for (const Rec& r : g_done) {
+    if (hipEventSynchronize(r.stop) != hipSuccess) rc = KFAC_ELAUNCH;
+    (void)hipEventDestroy(r.start);
+    (void)hipEventDestroy(r.stop);
+  }
+  for (hipEvent_t e : g_pool) (void)hipEventDestroy(e);
+  g_open.clear();
+  g_done.clear();
+  g_pool.clear();
+  return rc;
+}
+
 extern "C" int kfac_profile_reset(void) {
   std::lock_guard<std::mutex> lk(g_mu);
   for (const Rec& r : g_done) {

@@ -1483,6 +1483,13 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
     if (o.L % 4 != 0 || o.sB % 4 != 0 || reinterpret_cast<uintptr_t>(o.ptr) % 16 != 0 ||
         img / 4 > CONV_SRC_MAX)
       return false;
+    // a multi-batch job's float4 image loads start at every batch base (seg_ptrs is
+    // a host table): one misaligned base sends the job to the per-batch launches
+    if (nseg > 1) {
+      const float* const* bases = reinterpret_cast<const float* const*>(j.seg_ptrs);
+      for (int64_t s = 0; s < nseg; ++s)
+        if (reinterpret_cast<uintptr_t>(bases[s]) % 16 != 0) return false;
+    }
     const int segs = g.mode ? 4 * g.KR : g.KR;  // narrow: the 4 waves' segments too
     int Q = (int)cdiv(o.L, segs);
     if (g.mode >= 2) Q = (int)pad_to(Q, 16);
@@ -1776,7 +1783,7 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
       // 2- and 3-image tasks waited on the 3-image ones, and a CU running more
       // workgroups than another finished later (LeNet-5, batch 1024: conv2 A 68 us at
       // 400 splits -> 53 us at k = 2 (1,024 tasks); conv1 A 34 -> 27 us at k = 1;
-      // tools/microbench/conv_ab.hip, KFAC_CONV_K overrides k)
+      // `git show e37cdaa^:tools/microbench/conv_ab.hip`, KFAC_CONV_K overrides k)
       // (the n <= 8 channel kernel: half the slots -- its per-task reduction is the
       // larger cost there: conv1 G 15.7 / 12.4 / 13.2 us at k = 1 / 2 / 4)
       const bool small = jobs[i].x.layout == KFAC_CHANNEL && cg.n <= 8 && !conv_small_off();

@@ -132,6 +132,13 @@ extern "C" int kfac_invert(const kfac_invert_job* jobs, int njobs, void* workspa
   return kfac_invert_ex(jobs, njobs, workspace, workspace_bytes, info, nullptr, stream);
 }
 
+// the inversion's cached hipGraphs (both tile sizes); see kfac_release (capi.hip)
+int kfac_release_graphs() {
+  t64::release_graphs();
+  t32::release_graphs();
+  return KFAC_OK;
+}
+
 extern "C" int kfac_damped_inv_chol(const float* F, int n, int64_t ldF, double sqrt_s, double sqrt_n,
                                     float* L, int64_t ldL, void* workspace, size_t workspace_bytes,
                                     int32_t* info, kfac_stream_t stream) {

@@ -59,7 +59,9 @@ class DistributedKFAC(KFAC):
     `state`.  Reading `state` never communicates: it holds the reduced factors of
     the passes all-reduced so far (a read while this rank's pass is pending warns
     that the pass is not in it yet), so a rank-local read (`if rank == 0:
-    torch.save(kfac.state)`, logging) cannot deadlock the other ranks.
+    torch.save(kfac.state)`, logging) cannot deadlock the other ranks.  At world 1
+    (no collective) a `state` read sums the pending pass in itself; `save()` refuses
+    while a pass that needs the collective is pending.
 
     `shard_inversion`: "auto" (shard when world > 1 and some factor is larger than
     1536), True or False.
@@ -102,7 +104,11 @@ class DistributedKFAC(KFAC):
 
     @property
     def state(self):
-        """The all-reduced factors (no collective here; see the class docstring)."""
+        """The all-reduced factors (no collective here; see the class docstring).  With
+        no collective to run (world 1), a pending pass is summed in first: that is
+        purely local, so `update(); kfac.state` holds the whole pass as with KFAC."""
+        if getattr(self, "_pending", False) and not self._collective():
+            self.allreduce()
         if getattr(self, "_pending", False):
             import warnings
             warnings.warn("DistributedKFAC.state read while this rank's pass is not all-reduced "
@@ -115,6 +121,14 @@ class DistributedKFAC(KFAC):
     def state(self, value):
         self.flush()
         self._state = value
+
+    def save(self, filename):
+        """Curvature.save of the reduced state; refused while this rank's pass is not
+        all-reduced (the file would silently leave out the latest pass)."""
+        if getattr(self, "_pending", False) and self._collective():
+            raise RuntimeError("DistributedKFAC.save: this rank's pass is not all-reduced yet; call "
+                               "allreduce() (or invert()) on every rank first")
+        super().save(filename)
 
     def _collective(self):
         return self.world > 1 or self.always_reduce

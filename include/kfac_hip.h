@@ -326,6 +326,13 @@ KFAC_API int kfac_profile_read(int id, double* total_ms, int64_t* launches);
 KFAC_API int kfac_profile_reset(void);
 
 /* ------------------------------------------------------------------- misc */
+/* Release every HIP object the library keeps across calls (the inversion's cached
+ * hipGraphs and their events, the profiling event pool), waiting for their last
+ * use first.  Call before the HIP runtime shuts down (the Python binding registers
+ * it with atexit); later calls simply rebuild what they need.  No reference
+ * counterpart (the reference keeps no device state). */
+KFAC_API int kfac_release(void);
+
 KFAC_API const char* kfac_strerror(int status);
 KFAC_API const char* kfac_version(void);
 

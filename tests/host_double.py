@@ -119,11 +119,50 @@ def fake_invert(jobs, device, inputs_read=None):
 
 
 class HostEvent:
+    def __init__(self, *a, **k):
+        pass
+
+    def record(self, stream=None):
+        pass
+
     def query(self):
         return True
 
     def synchronize(self):
         pass
+
+
+class _HostStream:
+    def wait_stream(self, other):
+        pass
+
+    def wait_event(self, ev):
+        pass
+
+
+class _NoStream:
+    def __init__(self, stream=None):
+        pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+def install_cuda_stubs(kfac_list=()):
+    """Stand-ins for the torch.cuda stream / event calls of KFAC.invert (run with
+    overlap_invert False) so the plain single-device path runs on host memory; the
+    verdict readback of each KFAC in `kfac_list` uses an unpinned buffer."""
+    import torch
+    stream = _HostStream()
+    torch.cuda.current_stream = lambda device=None: stream
+    torch.cuda.stream = _NoStream
+    torch.cuda.Event = HostEvent
+    for k in kfac_list:
+        k.overlap_invert = False
+        k._pinned_info = lambda info: torch.empty(info.numel(), dtype=torch.int32)
 
 
 def install_distributed(kfac=None):

@@ -309,3 +309,55 @@ def test_sample_has_no_cpu_fallback():
         kfac.sample(net[0])
     with pytest.raises(N.NativeError):
         kfac.sample_and_replace()
+
+
+def test_distributed_world1_state_read_completes_pass(monkeypatch, tmp_path):
+    """DistributedKFAC at world 1 (no process group): `update(); kfac.state` holds the
+    whole pass, as with KFAC -- the pending pass needs no collective, so the read sums
+    it in (was: {} with a warning).  save() after it writes that state."""
+    import warnings
+    from bnn_kfac_amd.distributed import DistributedKFAC
+    host_double.install(monkeypatch)
+    net = mlp()
+    kfac = DistributedKFAC(net)
+    assert kfac.world == 1 and not kfac._collective()
+    ref = O.OracleKFAC(np.float64)
+    rng = np.random.default_rng(3)
+    for p in range(2):
+        for B in (7, 4):
+            a1 = rng.random((B, 6), dtype=np.float32)
+            g1 = rng.standard_normal((B, 5)).astype(np.float32)
+            a2 = rng.random((B, 5), dtype=np.float32)
+            g2 = rng.standard_normal((B, 3)).astype(np.float32)
+            kfac.record[net[0]] = [torch.from_numpy(a1), torch.from_numpy(g1)]
+            kfac.record[net[2]] = [torch.from_numpy(a2), torch.from_numpy(g2)]
+            kfac.update(B)
+            ref.update_linear("l0", a1, g1, True)
+            ref.update_linear("l1", a2, g2, True)
+        with warnings.catch_warnings():
+            warnings.simplefilter("error")  # no "not all-reduced" warning at world 1
+            st = kfac.state
+        assert not kfac._pending
+        np.testing.assert_allclose(st[net[0]][0].numpy(), ref.state["l0"][0], rtol=1e-5)
+        np.testing.assert_allclose(st[net[2]][1].numpy(), ref.state["l1"][1], rtol=1e-5)
+    kfac.save(str(tmp_path / "w1.pt"))  # (inv_state empty: nothing inverted)
+    blob = torch.load(str(tmp_path / "w1.pt"), weights_only=True)
+    np.testing.assert_allclose(blob["state"]["0"][0].numpy(), ref.state["l0"][0], rtol=1e-5)
+
+
+def test_distributed_save_refused_while_pass_pending(monkeypatch, tmp_path):
+    """With a collective to run (world > 1, modelled by always_reduce), save() refuses
+    while this rank's pass is not all-reduced instead of leaving it out silently."""
+    from bnn_kfac_amd.distributed import DistributedKFAC
+    host_double.install(monkeypatch)
+    net = mlp()
+    kfac = DistributedKFAC(net)
+    kfac.always_reduce = True
+    rng = np.random.default_rng(4)
+    kfac.record[net[0]] = [torch.from_numpy(rng.random((3, 6), dtype=np.float32)),
+                           torch.from_numpy(rng.standard_normal((3, 5)).astype(np.float32))]
+    kfac.record[net[2]] = [torch.from_numpy(rng.random((3, 5), dtype=np.float32)),
+                           torch.from_numpy(rng.standard_normal((3, 3)).astype(np.float32))]
+    kfac.update(3)
+    with pytest.raises(RuntimeError, match="not all-reduced"):
+        kfac.save(str(tmp_path / "x.pt"))

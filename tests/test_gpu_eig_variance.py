@@ -96,7 +96,14 @@ def test_classification_variance_golden(hip_device):
 
 
 def test_regression_variance_golden(hip_device):
-    """G7: regression block, pinv(N(q + tau I)) (x) pinv(N(h + tau I)) on device."""
+    """G7: regression block, pinv(N(q + tau I)) (x) pinv(N(h + tau I)) on device
+    (sampling_free/regression/regression_ll_block.py:125-140).
+
+    Judged at the north-star tolerance against the fp64 oracle on the same state:
+    every per-layer v and std at rtol 1e-4 (O.spd_inverse_scaled + O.kron_quadform).
+    The reference's own fp32 outputs sit up to 2.3e-4 (v) / 3.2e-5 (std) from that
+    fp64 truth (cond(q + tau I) ~3.2e3; measured on this fixture, and re-asserted
+    below), so the fixture check runs at that band: rtol 5e-4 on v."""
     from bnn_kfac_amd.curvatures import KFAC
     from bnn_kfac_amd.variance import kron_quadform, regression_inverse_factors
     g = golden("g7_regression.npz")
@@ -111,7 +118,14 @@ def test_regression_variance_golden(hip_device):
     for j in range(len(g["xs"])):
         terms = [(_t(g[f"J_{j}_{li}"], hip_device), inv[li][0], inv[li][1]) for li in range(3)]
         out, v = kron_quadform(terms, lower=False, per_term=True)
-        np.testing.assert_allclose(v.cpu().numpy()[:, 0], g["v"][j], rtol=2e-3, atol=1e-7)
+        v = v.cpu().numpy()[:, 0]
+        want = np.array([O.kron_quadform(g[f"J_{j}_{li}"], O.spd_inverse_scaled(g[f"q{li}"], N, N * tau),
+                                         O.spd_inverse_scaled(g[f"h{li}"], N, N * tau))[0] for li in range(3)])
+        np.testing.assert_allclose(v, want, rtol=1e-4, atol=0)
+        np.testing.assert_allclose(float(out[0]) ** 0.5 + sigma, want.sum() ** 0.5 + sigma, rtol=1e-4)
+        # the reference's fp32 pipeline vs the same fp64 truth: its own error band
+        assert np.max(np.abs(g["v"][j] - want) / np.abs(want)) <= 2.5e-4
+        np.testing.assert_allclose(v, g["v"][j], rtol=5e-4, atol=0)
         np.testing.assert_allclose(float(out[0]) ** 0.5 + sigma, g["std"][j], rtol=1e-4)
 
 
