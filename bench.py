@@ -405,6 +405,9 @@ def main(argv=None):
     ap.add_argument("--single-buffer", action="store_true",
                     help="KFAC.double_buffer = False (the data stream waits for each "
                          "inversion to have read its factors)")
+    ap.add_argument("--host-profile", default=None,
+                    help="diagnostic: after the timed region, run --steps more pipelined steps under "
+                         "cProfile and write the host-side statistics (tottime) to this file")
     ap.add_argument("--no-parity", action="store_true",
                     help="N > 1: skip the post-timing verification pass (verify_parity)")
     ap.add_argument("--shared-device", action="store_true",
@@ -531,6 +534,32 @@ def main(argv=None):
     kfac.inv_state
     sync()
     elapsed = max_over_ranks(time.perf_counter() - t0)
+
+    if args.host_profile:
+        import cProfile
+        import io
+        import pstats
+        pr = cProfile.Profile()
+        t1 = time.perf_counter()
+        pr.enable()
+        for _ in range(args.steps):
+            one_pass()
+        pr.disable()
+        t_prof = time.perf_counter() - t1
+        kfac.inv_state
+        sync()
+        out = io.StringIO()
+        out.write(f"{args.steps} pipelined steps issued in {1e3 * t_prof / args.steps:.3f} ms/step under cProfile "
+                  f"(unprofiled host issue {1e3 * t_issue / args.steps:.3f} ms/step)\n")
+        # per step, in microseconds (pstats' own listing rounds to milliseconds)
+        st = pstats.Stats(pr).stats
+        for key, label in ((3, "cumulative"), (2, "own")):
+            out.write(f"\n-- {label} us per step --\n")
+            for fn, v in sorted(st.items(), key=lambda kv: -kv[1][key])[:35]:
+                out.write(f"{1e6 * v[key] / args.steps:9.1f} us  {v[1] / args.steps:6.1f} calls  "
+                          f"{os.path.basename(fn[0])}:{fn[1]}({fn[2]})\n")
+        with open(args.host_profile, "w") as f:
+            f.write(out.getvalue())
 
     # Kernel durations: the same K steps again with the library's HIP-event timing
     # on (events recorded around each launch, on its stream).  Kept out of the timed

@@ -42,3 +42,11 @@ def main():
 
 if __name__ == "__main__":
     main()
+    if os.environ.get("EIG_FAST_EXIT") == "1":
+        # profiler passes: a process that ran a cooperative launch (eig_tridiag)
+        # segfaults in exit() after rocprofv3 --pmc's tool finalization (not without
+        # --pmc, not without the cooperative launch: tools/exit_probe.py, DESIGN.md
+        # §3.4); leave without the exit handlers once the output is flushed
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)

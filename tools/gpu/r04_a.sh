@@ -20,4 +20,6 @@ export EIG_NO_CPU=1
 cd /tmp
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $GRAFT_REPO_ROOT/$O/eig_fetch -o run -- python3 $GRAFT_REPO_ROOT/tools/bench_eig.py 4097 > $GRAFT_REPO_ROOT/$O/eig_fetch.log 2>&1; echo "eig under pmc: rc $?"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $GRAFT_REPO_ROOT/$O/ctl_fetch -o run -- python3 $GRAFT_REPO_ROOT/tools/exit_control.py > $GRAFT_REPO_ROOT/$O/ctl_fetch.log 2>&1; echo "control under pmc: rc $?"
+cd $GRAFT_REPO_ROOT
+timeout -k 10 90 ./tools/microbench/x3w_mb > $O/x3w_mb.log 2>&1; echo "x3w_mb rc $?"; cat $O/x3w_mb.log
 exit 0
