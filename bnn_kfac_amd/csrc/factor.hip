@@ -791,87 +791,192 @@ __device__ __forceinline__ X3Frag x3_split8(const float (&x)[8]) {
   return f;
 }
 
-template <int MASK>
-__device__ __forceinline__ void x3_loop_direct(const FactorJobDev& J, const float* const* segs, int ti, int tj,
-                                               int64_t s0, int64_t s1, floatx16 (&acc)[2][2]) {
+// The stage loop (round 4): software-pipelined segments in ONE straight-line block.
+// The fragments of the stage's first block -- A0 (and B0) -- are split during the
+// previous stage; every segment is the six MFMAs of one block interleaved
+// (sched_group_barrier) with the split of a fragment a later block needs, and that
+// fragment's registers are reloaded as soon as its split has read them:
+//   full tile (mask 15):  (0,0) | split A1    (1,0) | split B1    (0,1) | split A0'
+//                         (1,1) | split B0'
+// so each load goes out one whole stage before its split (x1, x3 hold the next stage,
+// x0, x2 the one after), at most five fragments are live and no register set is copied
+// (2 waves per SIMD at <= 200 VGPRs leave an inversion wave room beside them).  Round 3's
+// loop split all four fragments at the top of the stage, copied a 32-register prefetch
+// set into the working set every stage, branched per stage (last stage, batch change,
+// fill columns with 64-bit compares), and the compiler sank every load to the end of
+// the body and waited vmcnt(0) at the loop head: ~100 extra VALU and the whole L2
+// latency per stage.  Now every load is unconditional: past the task's range the
+// cursor stops (the last stage reloads itself), a batch change is a scalar select (the
+// next batch's base fetched a stage ahead), columns past the operand load from past
+// the buffer's record limit (0), and the ones column (FILL: only the tasks whose
+// fragments hold it) is a select of 1 / 0 by row validity.
+// Microbench: tools/microbench/x3w_mb.hip; DESIGN.md §3.1c.
+struct X3Cursor {  // a stage to load: batch `seg` (base `b`), first row `k`
+  const float* b;
+  int seg, k;
+};
+
+template <int NV>
+__device__ __forceinline__ void x3_pattern() {  // 6 MFMAs, NV VALU each, the reloads early
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);       // MFMA
+    if (NV > 0) __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);  // VALU
+    if (i < 4) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);    // VMEM read
+  }
+}
+
+template <int MASK, bool FILL>
+__device__ __forceinline__ void x3_loop(const FactorJobDev& J, const float* const* segs, int ti, int tj,
+                                        int64_t s0, int64_t s1, floatx16 (&acc)[2][2]) {
   constexpr bool A00 = MASK & 1, A01 = MASK & 2, A10 = MASK & 4, A11 = MASK & 8;
   constexpr bool ROW1 = A10 || A11, COL1 = A01 || A11;
   // masks 13 and 1 occur on diagonal tiles only (an off-diagonal tile with block
   // (1, 1), or with any block, has (0, 1)): B fragments = A fragments
   constexpr bool SAME = MASK == 13 || MASK == 1;
+  static_assert(A00, "block (0, 0) always has work");
   // fragments: 0 A block 0, 1 A block 1, 2 B block 0, 3 B block 1
   constexpr bool USE[4] = {true, ROW1, !SAME, !SAME && COL1};
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ld4 = (int)J.x.ld * 4;
+  const int rows = (int)J.x.rows;
+  const int rec = rows * ld4;                  // a batch's bytes (planner: < 2^31)
   const int lr = 16 * wave + 8 * (lane >> 5);  // lane's first row within a stage
-  X3Col col[4];
-  bool anyfill = false;
+  int voff[4];
+  bool onesl[4];
 #pragma unroll
   for (int f = 0; f < 4; ++f) {
     const int c = (f < 2 ? ti : tj) * TILE + (f & 1) * 32 + (lane & 31);
-    col[f].fill = c >= J.x.cols;
-    col[f].fv = c == J.x.ones ? 1.f : 0.f;
-    col[f].voff = lr * ld4 + (col[f].fill ? 0 : c) * 4;
-    if (USE[f]) anyfill |= (f < 2 ? ti : tj) * TILE + (f & 1) * 32 + 31 >= J.x.cols;
+    voff[f] = c < J.x.cols ? lr * ld4 + c * 4 : rec;  // past the operand: the zero tail
+    onesl[f] = c == J.x.ones;
   }
-  const int64_t rows = J.x.rows;
   const int ns = (int)(s1 - s0);
-  StageCursor ic;
-  ic.init(J, s0);
-  int cseg = ic.seg;
-  auto rsrc = [&](int seg) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(seg_base(J, segs, seg)), 0,
-                                             (int)(rows * ld4), 0x00020000);
+  const int lastseg = J.nseg - 1;
+  // stage cursors: c1 = the next stage to load for fragments 1 / 3, c2 = the one after
+  // (fragments 0 / 2); nb = the base of the batch after c2's
+  X3Cursor c2;
+  c2.seg = (int)(s0 / J.sps);
+  c2.k = (int)((s0 - (int64_t)c2.seg * J.sps) * BK);
+  c2.b = seg_base(J, segs, c2.seg);
+  const float* nb = seg_base(J, segs, min(c2.seg + 1, lastseg));
+  int left = ns - 1;  // stages after c2's within the task (the cursor stops at the last)
+  auto advance = [&](X3Cursor& c) {
+    const bool more = left > 0;
+    const bool wrap = more && c.k + BK >= rows;
+    c.k = more ? (wrap ? 0 : c.k + BK) : c.k;
+    c.seg += wrap;
+    c.b = wrap ? nb : c.b;
+    nb = seg_base(J, segs, min(c.seg + 1, lastseg));
+    left -= more;
   };
-  __amdgpu_buffer_rsrc_t rs = rsrc(cseg);
-  float xn[4][8];
-  int64_t kn = ic.k;  // first row of the loaded stage
-  auto load = [&]() {
-    if (ic.seg != cseg) {
-      cseg = ic.seg;
-      rs = rsrc(cseg);
-    }
-    kn = ic.k;
-    const int sb = (int)ic.k * ld4;
-#pragma unroll
-    for (int f = 0; f < 4; ++f)
-      if (USE[f]) x3_load8(xn[f], rs, col[f], sb, ld4);
-    ic.next(rows);
+  auto rsrc = [&](const float* b) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(b), 0, rec, 0x00020000);
   };
-  load();
-  for (int st = 0; st < ns; ++st) {
-    float x[4][8];
+  auto ld8 = [&](int f, const X3Cursor& c, float (&x)[8]) {
+    x3_load8(x, rsrc(c.b), X3Col{voff[f], false, 0.f}, c.k * ld4, ld4);
+  };
+  float x[4][8];
+  // prologue: stage s0 into every fragment, the first block's fragments split, their
+  // registers reloaded with stage s0 + 1
+  const int k0 = c2.k;
 #pragma unroll
-    for (int f = 0; f < 4; ++f)
+  for (int f = 0; f < 4; ++f)
+    if (USE[f]) ld8(f, c2, x[f]);
+  advance(c2);
+  X3Cursor c1 = c2;  // (fragments 1 / 3 load stage s0 + 1 in the first stage)
+  int kc = k0;       // first row of the stage being multiplied
+  auto fix = [&](int f, int kstage) {  // the ones column: 1 on the batch's rows, 0 past them
+    if constexpr (FILL) {
+      const int nvalid = rows - kstage;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) x[f][r] = xn[f][r];
-    const int64_t kc = kn;
-    if (st + 1 < ns) load();
-    if (anyfill) {  // columns past the data: their fill (rows past the batch: 0)
-#pragma unroll
-      for (int f = 0; f < 4; ++f)
-        if (USE[f] && col[f].fill)
-#pragma unroll
-          for (int r = 0; r < 8; ++r) x[f][r] = kc + lr + r < rows ? col[f].fv : 0.f;
+      for (int r = 0; r < 8; ++r) x[f][r] = onesl[f] ? (lr + r < nvalid ? 1.f : 0.f) : x[f][r];
     }
-    const X3Frag A0 = x3_split8(x[0]);
-    const X3Frag B0 = SAME ? A0 : x3_split8(x[2]);
-    if constexpr (A00) x3_six(acc[0][0], A0, B0);
-    if constexpr (ROW1) {
-      const X3Frag A1 = x3_split8(x[1]);
-      if constexpr (A10) x3_six(acc[1][0], A1, B0);
-      if constexpr (COL1) {
-        const X3Frag B1 = SAME ? A1 : x3_split8(x[3]);
-        if constexpr (A01) x3_six(acc[0][1], A0, B1);
-        if constexpr (A11) x3_six(acc[1][1], A1, B1);
-      }
-    } else if constexpr (COL1) {
-      const X3Frag B1 = x3_split8(x[3]);
+  };
+  // split fragment f (of the stage starting at row kstage) and reload its registers
+  auto take = [&](int f, int kstage, const X3Cursor& c) {
+    fix(f, kstage);
+    const X3Frag fr = x3_split8(x[f]);
+    ld8(f, c, x[f]);
+    return fr;
+  };
+  X3Frag pa = take(0, k0, c2);
+  X3Frag pb = SAME ? pa : take(2, k0, c2);
+  // the prologue's loads complete here (once per task): the loop header then starts
+  // from a precise wait state, and the compiler keeps the counted vmcnt at the top of
+  // each stage (with the prologue's loads still in flight it merged them into a
+  // vmcnt(0) there, exposing a whole stage of load latency)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  constexpr int NV = FILL ? 52 / 6 + 1 : 44 / 6 + 1;
+  // one stage: P = (A0, B0) of this stage in, (A0', B0') of the next stage out
+  auto stage = [&](const X3Frag& A0, const X3Frag& B0, X3Frag& A0n, X3Frag& B0n) {
+    const int kn = c2.k;  // first row of the next stage (in x0 / x2 now)
+    // the cursors: x1 / x3 reload the next stage, x0 / x2 the one after
+    c1 = c2;
+    advance(c2);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (MASK == 15) {
+      const X3Frag A1 = take(1, kc, c1);
+      x3_six(acc[0][0], A0, B0);
+      x3_pattern<NV>();
+      __builtin_amdgcn_sched_barrier(0);
+      const X3Frag B1 = take(3, kc, c1);
+      x3_six(acc[1][0], A1, B0);
+      x3_pattern<NV>();
+      __builtin_amdgcn_sched_barrier(0);
+      A0n = take(0, kn, c2);
       x3_six(acc[0][1], A0, B1);
+      x3_pattern<NV>();
+      __builtin_amdgcn_sched_barrier(0);
+      B0n = take(2, kn, c2);
+      x3_six(acc[1][1], A1, B1);
+      x3_pattern<NV>();
+    } else if constexpr (MASK == 13) {  // diagonal: (0,0) (1,0) (1,1), B = A
+      const X3Frag A1 = take(1, kc, c1);
+      x3_six(acc[0][0], A0, A0);
+      x3_pattern<NV>();
+      __builtin_amdgcn_sched_barrier(0);
+      x3_six(acc[1][0], A1, A0);
+      A0n = take(0, kn, c2);
+      x3_pattern<NV>();
+      __builtin_amdgcn_sched_barrier(0);
+      x3_six(acc[1][1], A1, A1);
+      x3_pattern<0>();
+      B0n = A0n;
+    } else if constexpr (MASK == 5) {  // (0,0) (1,0)
+      const X3Frag A1 = take(1, kc, c1);
+      x3_six(acc[0][0], A0, B0);
+      x3_pattern<NV>();
+      __builtin_amdgcn_sched_barrier(0);
+      A0n = take(0, kn, c2);
+      B0n = take(2, kn, c2);
+      x3_six(acc[1][0], A1, B0);
+      x3_pattern<2 * NV>();
+    } else if constexpr (MASK == 3) {  // (0,0) (0,1): the last tile row of a factor
+      const X3Frag B1 = take(3, kc, c1);
+      x3_six(acc[0][0], A0, B0);
+      x3_pattern<NV>();
+      __builtin_amdgcn_sched_barrier(0);
+      A0n = take(0, kn, c2);
+      B0n = take(2, kn, c2);
+      x3_six(acc[0][1], A0, B1);
+      x3_pattern<2 * NV>();
+    } else {  // 1: the last diagonal tile, (0,0) only, B = A
+      A0n = take(0, kn, c2);
+      x3_six(acc[0][0], A0, A0);
+      x3_pattern<NV>();
+      B0n = A0n;
     }
+    kc = kn;
+  };
+  for (int st = 0; st < ns; ++st) {
+    X3Frag qa, qb;
+    stage(pa, pb, qa, qb);
+    pa = qa;
+    pb = qb;
   }
 }
+
 template <int GBK, int NSLOT>
 __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const float* const* segs, int local,
                                                float* lds, int split_major) {
@@ -903,14 +1008,23 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[bi][bj][v] = 0.f;
   if (s1 > s0) {
+    // FILL: one of the task's fragments holds the ones column (the last tile row /
+    // column of an A factor with a bias)
+    const bool fill = J.x.ones >= 0 && ((J.x.ones >> 6) == ti || (J.x.ones >> 6) == tj);
+#define X3_CASE(M)                                                   \
+  case M:                                                            \
+    if (fill) x3_loop<M, true>(J, segs, ti, tj, s0, s1, acc);        \
+    else x3_loop<M, false>(J, segs, ti, tj, s0, s1, acc);            \
+    break;
     switch (mask) {  // (block (0, 0) always has work)
-      case 15: x3_loop_direct<15>(J, segs, ti, tj, s0, s1, acc); break;
-      case 13: x3_loop_direct<13>(J, segs, ti, tj, s0, s1, acc); break;  // diagonal
-      case 5: x3_loop_direct<5>(J, segs, ti, tj, s0, s1, acc); break;
-      case 3: x3_loop_direct<3>(J, segs, ti, tj, s0, s1, acc); break;
-      case 1: x3_loop_direct<1>(J, segs, ti, tj, s0, s1, acc); break;
-      default: x3_loop_direct<15>(J, segs, ti, tj, s0, s1, acc); break;  // (not reached)
+      X3_CASE(15)
+      X3_CASE(13)  // diagonal
+      X3_CASE(5)
+      X3_CASE(3)
+      X3_CASE(1)
+      default: break;  // (not reached)
     }
+#undef X3_CASE
   }
   // wave w stores block row w: it hands the other block row's partials to the other
   // wave through LDS (the ring is free after the barrier), then adds the other

@@ -231,6 +231,7 @@ class KFAC(Curvature):
         self._acc_flush = None   # flush jobs of the pending cycle (None: nothing pending)
         self._acc_device = None
         self._info_pool = []     # free pinned int32 readback buffers of the pivot checks
+        self._event_pool = {}    # device index -> settled torch.cuda.Events (no event creation per invert)
         self._inv_older = []     # earlier inversions whose verdict is not read yet (in order)
         self._inv_pending = None  # _Pending of the last inversion until its verdict is settled
         self.overlap_invert = True  # invert() on a side stream (see invert)
@@ -266,6 +267,7 @@ class KFAC(Curvature):
         ev = self._buf_read.pop(buf.data_ptr(), None)
         if ev is not None:
             (stream or torch.cuda.current_stream(buf.device)).wait_event(ev)
+            self._pool_event(buf.device, ev)  # the wait captured its record: reusable
 
     def flush(self):
         """Launch queued updates, then reduce the pending accumulators into the
@@ -401,8 +403,9 @@ class KFAC(Curvature):
     def update(self, batch_size: int):
         """Accumulate this batch's factors for every selected layer
         (curvatures.py:325-365; `batch_size` is unused there too)."""
-        if self.defer_reduce and self._fast is not None:
-            entry = self._fast_entry()
+        fast = self._fast
+        if fast is not None and self.defer_reduce:
+            entry = self._fast_entry(fast)
             if entry is not None:
                 self._enqueue(entry)
                 return
@@ -467,8 +470,8 @@ class KFAC(Curvature):
         self._fast_bytes = sum(t.numel() * t.element_size()
                                for layer, *_ in prepared for t in self.record[layer])
 
-    def _fast_entry(self):
-        scale, spec, tmpl, device = self._fast
+    def _fast_entry(self, fast):
+        scale, spec, tmpl, device = fast
         if getattr(self, "_scale", 1.0) != scale:
             return None
         record, state = self.record, self._state
@@ -491,7 +494,8 @@ class KFAC(Curvature):
     def _enqueue(self, entry):
         """Queue one update: (jobs, operand pointers, records kept alive, their
         _version, device, merge key)."""
-        if self._queue and self._queue[0][4] != entry[4]:
+        queue = self._queue
+        if queue and queue[0][4] is not entry[4] and queue[0][4] != entry[4]:
             self._launch_queue()
         self._queue.append(entry)
         fast = self._fast
@@ -630,7 +634,7 @@ class KFAC(Curvature):
         read = None
         if side is not main:
             side.wait_stream(main)
-            read = torch.cuda.Event()
+            read = self._event(device)
             read.record(side)  # creates the event; kfac_invert_ex records it again
         outs, jobs = [], []
         with torch.cuda.stream(side):
@@ -648,7 +652,7 @@ class KFAC(Curvature):
             # invert(), so a data pass can be queued behind this inversion.
             host = self._pinned_info(info)
             host.copy_(info, non_blocking=True)
-            done = torch.cuda.Event()
+            done = self._event(device)
             done.record(side)
         if read is not None:
             self._release(main, read, entries)
@@ -658,6 +662,15 @@ class KFAC(Curvature):
                                      [t for _, pair in outs for t in pair], side is not main)
         if self.eager_verdict:
             self._check_inverse()
+
+    def _event(self, device):
+        """A torch.cuda.Event from the pool of settled ones (a verdict's `done` after
+        its host wait, an inputs-read event after the wait on it was enqueued)."""
+        pool = self._event_pool.get(device.index)
+        return pool.pop() if pool else torch.cuda.Event()
+
+    def _pool_event(self, device, ev):
+        self._event_pool.setdefault(device.index, []).append(ev)
 
     def _pinned_info(self, info):
         """A pinned host int32 buffer for a verdict readback (pooled)."""
@@ -677,6 +690,7 @@ class KFAC(Curvature):
                 self._buf_read[buf.data_ptr()] = read
                 return
         main.wait_event(read)
+        self._pool_event(main.device, read)
 
     def _side_stream(self, device, alternate=True):
         """The side stream of this inversion: two high-priority streams taken in turn,
@@ -743,6 +757,8 @@ class KFAC(Curvature):
         pending.done.synchronize()
         bad = pending.host.numpy().copy()
         self._info_pool.append(pending.host)
+        if pending.outs:
+            self._pool_event(pending.outs[0].device, pending.done)
         if bad.any():
             first = int(np.flatnonzero(bad)[0]) // 2  # two jobs (A, G) per layer
             for layer in pending.layers[first:]:
