@@ -972,16 +972,36 @@ class INF(Curvature):
         return INF._pre_sample_from_gram(vtv, reg_lambda)
 
     @staticmethod
-    def _pre_sample_from_gram(vtv: Tensor, reg_lambda: Tensor) -> Tensor:
-        """curvatures.py:567-580 on the scaled Gram matrix (the reference's symmetrisation,
-        then its Cholesky / inverse sequence)."""
+    def _pre_sample_from_gram(vtv: Tensor, reg_lambda: Tensor, chol_inverse=None) -> Tensor:
+        """curvatures.py:567-580 on the scaled Gram matrix.  The reference forms
+        A = chol(vtv)^-1, B = chol(vtv + I), C = A^T (B - I) A and L_c = (C^-1 + vtv)^-1
+        with two general inverses.  With vtv = L L^T, C^-1 = L (B - I)^-1 L^T, so
+        C^-1 + vtv = L (B - I)^-1 B L^T and
+            L_c = A^T (I - B^-1) A
+        -- the same matrix from two triangular Cholesky inverses (kfac_invert on the
+        device, fp64 inside: _chol_inverse) and two GEMMs, no general inverse.  On the
+        reference's own G11 inputs it is 1e-12 from the fp64 literal chain and <= 8e-7
+        with fp32 factors and GEMMs, where the reference's fp32 chain is up to 1.4e-4 off
+        (cond(vtv) ~2e5 at full rank)."""
         vtv = (vtv + vtv.t()) / 2.
         eye = torch.eye(vtv.shape[0], device=vtv.device, dtype=vtv.dtype)
-        A_c_inv = torch.linalg.cholesky(vtv).inverse()
-        B_c = torch.linalg.cholesky(vtv + eye)
-        C = A_c_inv.t() @ (B_c - eye) @ A_c_inv
-        L_c = (C.inverse() + vtv).inverse()
+        A, B_inv = (chol_inverse or INF._chol_inverse)(vtv, (0.0, 1.0))
+        L_c = A.t() @ (eye - B_inv) @ A
         return reg_lambda[:, None] * L_c * reg_lambda[None, :]
+
+    @staticmethod
+    def _chol_inverse(R: Tensor, shifts) -> list:
+        """[chol(R + t I)^-1 for t in shifts] (lower) by ONE grouped kfac_invert: it
+        computes X = chol(P R' P)^-1 and returns L = P X^T P (P the exchange matrix),
+        so with R' = P R P (the flipped input) X = chol(R)^-1 = P L^T P."""
+        N.require_device(R, "INF Gram matrix")
+        Rf = torch.flip(R, (0, 1)).contiguous()
+        outs = [torch.empty_like(Rf) for _ in shifts]
+        info = N.invert([N.invert_job(Rf, o, 1.0, float(t)) for o, t in zip(outs, shifts)], R.device)
+        if bool(info.any()):  # torch.linalg.cholesky's error in the reference
+            raise RuntimeError("cholesky: The factorization could not be completed because the input "
+                               "is not positive-definite.")
+        return [torch.flip(o, (0, 1)).t() for o in outs]
 
     @staticmethod
     def sampler(frst_eigvecs: Tensor, scnd_eigvecs: Tensor, reg_inv_correction: Tensor,

@@ -262,6 +262,13 @@ def test_variance_helpers():
     assert abs(entropy_bits(1.0) - 0.5 * np.log2(2 * np.e * np.pi)) < 1e-12
 
 
+def _host_chol_inverse(R, shifts):
+    """Host test double of INF._chol_inverse (kfac_invert on the device)."""
+    import torch
+    eye = torch.eye(R.shape[0], dtype=R.dtype)
+    return [torch.linalg.inv(torch.linalg.cholesky(R + t * eye)) for t in shifts]
+
+
 def test_inf_host_algebra_matches_literal_oracle():
     """INF's tensor restatements (curvatures.py:614-682: index arithmetic, the per-row
     kron loop; :548-580 the pre-sample after the Gram matrix) against the literal
@@ -290,7 +297,8 @@ def test_inf_host_algebra_matches_literal_oracle():
         # the pre-sample's linear algebra after the Gram matrix (the Gram itself is
         # kfac_kron_gram on the device: pre_sampler has no host path)
         Vs = c[:, None] * np.kron(wa, wb) * sig[None, :]
-        P = INF._pre_sample_from_gram(torch.from_numpy(Vs.T @ Vs), torch.from_numpy(sig)).numpy()
+        P = INF._pre_sample_from_gram(torch.from_numpy(Vs.T @ Vs), torch.from_numpy(sig),
+                                      chol_inverse=_host_chol_inverse).numpy()
         np.testing.assert_allclose(P, O.inf_pre_sampler(wa, wb, sig, c), rtol=1e-8, atol=1e-12)
         with pytest.raises(N.NativeError):
             INF.pre_sampler(a, b, torch.from_numpy(sig), torch.from_numpy(c))

@@ -78,7 +78,9 @@ def _pre_sample(a, b, sig, c):
     from bnn_kfac_amd.curvatures import INF
     Vs = c.double().numpy()[:, None] * np.kron(a.double().numpy(), b.double().numpy()) * sig.double().numpy()[None, :]
     gram = torch.from_numpy(Vs.T @ Vs).to(a.dtype)
-    return INF._pre_sample_from_gram(gram, sig)
+    eye = torch.eye(gram.shape[0], dtype=gram.dtype)
+    return INF._pre_sample_from_gram(  # (host test double of the device Cholesky inverses)
+        gram, sig, chol_inverse=lambda R, ts: [torch.linalg.inv(torch.linalg.cholesky(R + t * eye)) for t in ts])
 
 
 @pytest.mark.parametrize("li", [0, 1])

@@ -172,3 +172,22 @@ def test_kron_gram_vs_explicit_kron(hip_device, nA, nG, la, lg):
     want = sig[:, None] * (Vs.T @ Vs) * sig[None, :]
     np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-5 * np.abs(want).max())
     np.testing.assert_allclose(got, got.T, rtol=2.5e-7, atol=0)
+
+
+@pytest.mark.parametrize("n", [1, 15, 33, 196, 700])
+def test_inf_chol_inverse_device(hip_device, n):
+    """INF._chol_inverse: chol(R + t I)^-1 for t in (0, 1) by one grouped kfac_invert on
+    the flipped input, against fp64 inv(cholesky(.)) (the reference's
+    vtv.cholesky().inverse() and (vtv + I).cholesky(), curvatures.py:574-576)."""
+    from bnn_kfac_amd.curvatures import INF
+    rng = np.random.default_rng(n)
+    X = rng.standard_normal((2 * n + 3, n))
+    R = (X.T @ X / n).astype(np.float32)
+    A, B_inv = INF._chol_inverse(torch.from_numpy(R).to(hip_device), (0.0, 1.0))
+    for got, t in ((A, 0.0), (B_inv, 1.0)):
+        want = np.linalg.inv(np.linalg.cholesky(R.astype(np.float64) + t * np.eye(n)))
+        got = got.cpu().numpy()
+        np.testing.assert_allclose(got, want, rtol=0, atol=1e-5 * np.abs(want).max())
+        assert np.all(np.triu(got, 1) == 0)
+    with pytest.raises(RuntimeError, match="positive-definite"):
+        INF._chol_inverse(torch.zeros(n, n, device=hip_device) - 1.0, (0.0,))
