@@ -126,6 +126,14 @@ SIGNATURES = {
                                          ctypes.POINTER(ctypes.c_int64)]),
     "kfac_profile_reset": (ctypes.c_int, []),
     "kfac_release": (ctypes.c_int, []),
+    "kfac_invert_pipelined": (ctypes.c_int, [ctypes.POINTER(InvertJob), ctypes.c_int, c_vp, ctypes.c_size_t,
+                                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "kfac_event_create": (ctypes.c_int, [ctypes.POINTER(c_vp)]),
+    "kfac_event_destroy": (ctypes.c_int, [c_vp]),
+    "kfac_event_record": (ctypes.c_int, [c_vp, c_vp]),
+    "kfac_stream_wait_event": (ctypes.c_int, [c_vp, c_vp]),
+    "kfac_event_query": (ctypes.c_int, [c_vp]),
+    "kfac_event_synchronize": (ctypes.c_int, [c_vp]),
     "kfac_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "kfac_version": (ctypes.c_char_p, []),
 }
@@ -163,9 +171,44 @@ def lib():
 def _release_at_exit():
     try:
         if _lib is not None and torch.cuda.is_initialized():
+            for h in _raw_events:
+                _lib.kfac_event_destroy(h)
+            _raw_events.clear()
             _lib.kfac_release()
     except Exception:  # exiting anyway: never mask the process's own status
         pass
+
+
+_raw_events = []  # handles of every RawEvent made (destroyed at exit, while HIP is up)
+
+
+class RawEvent:
+    """A HIP event owned through the C ABI (kfac_event_*): record / wait / query /
+    synchronize are one ctypes call each, where torch.cuda.Event and Stream objects
+    cost the caller's thread 5-10 us per call.  Kept for the process (pooled)."""
+    __slots__ = ("handle",)
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        check(lib().kfac_event_create(ctypes.byref(h)), "kfac_event_create")
+        self.handle = h.value
+        _raw_events.append(self.handle)
+
+    def record(self, stream: int):
+        check(_lib.kfac_event_record(self.handle, stream), "kfac_event_record")
+
+    def wait_on(self, stream: int):
+        """Order `stream`'s later work after this event's recorded work."""
+        check(_lib.kfac_stream_wait_event(stream, self.handle), "kfac_stream_wait_event")
+
+    def query(self) -> bool:
+        r = _lib.kfac_event_query(self.handle)
+        if r < 0:
+            check(r, "kfac_event_query")
+        return r == 1
+
+    def synchronize(self):
+        check(_lib.kfac_event_synchronize(self.handle), "kfac_event_synchronize")
 
 
 def check(rc: int, what: str):
@@ -203,11 +246,18 @@ class _Workspace:
     def __init__(self):
         self._bufs = {}
 
-    def get(self, device: torch.device, nbytes: int, stream: int = None) -> torch.Tensor:
+    def get(self, device: torch.device, nbytes: int, stream: int = None, stream_obj=None) -> torch.Tensor:
+        """`stream_obj`: the torch stream the work runs on when it is not the current one
+        -- a (re)allocation is then made on it, so the caching allocator orders a grown
+        buffer's release after that stream's queued work, not the current stream's."""
         key = (device.index, stream_handle(device) if stream is None else stream)
         buf = self._bufs.get(key)
         if buf is None or buf.numel() < nbytes:
-            buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+            if stream_obj is not None:
+                with torch.cuda.stream(stream_obj):
+                    buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+            else:
+                buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
             self._bufs[key] = buf
         return buf
 
@@ -273,6 +323,26 @@ def invert(jobs, device: torch.device, inputs_read=None) -> torch.Tensor:
         ev = inputs_read.cuda_event
     check(L.kfac_invert_ex(arr, len(jobs), ws.data_ptr(), ws.numel(), info.data_ptr(), ev, stream),
           "kfac_invert_ex")
+    return info
+
+
+def invert_pipelined(jobs, device: torch.device, info_host: torch.Tensor, order: "RawEvent",
+                     inputs_read, done: "RawEvent", main: int, side: int, side_stream=None) -> torch.Tensor:
+    """kfac_invert_pipelined: `side` ordered after `main`, the grouped inversion on `side`
+    (`inputs_read` recorded after the F-reading launch), the verdict copied into the
+    pinned `info_host`, `done` recorded on `side`.  Returns the device verdict vector."""
+    L = lib()
+    arr = as_array(InvertJob, jobs)
+    need = L.kfac_invert_workspace_bytes(arr, len(jobs))
+    ws = workspace.get(device, need, side, side_stream)
+    key = (device.index, side, len(jobs))
+    info = _info_bufs.get(key)
+    if info is None:
+        info = _info_bufs[key] = torch.empty(len(jobs), dtype=torch.int32, device=device)
+    check(L.kfac_invert_pipelined(arr, len(jobs), ws.data_ptr(), ws.numel(), info.data_ptr(),
+                                  info_host.data_ptr(), order.handle,
+                                  inputs_read.handle if inputs_read is not None else None,
+                                  done.handle, main, side), "kfac_invert_pipelined")
     return info
 
 

@@ -115,6 +115,33 @@ extern "C" int kfac_release(void) {
   return rc;
 }
 
+// ---------------------------------------------------------------- raw events / streams
+// The host side's ordering primitives without torch.cuda's Python objects (each of
+// those calls costs the caller's thread 5-10 us; these are one ctypes call each).
+extern "C" int kfac_event_create(void** ev) {
+  if (!ev) return KFAC_EINVAL;
+  return hipEventCreateWithFlags(reinterpret_cast<hipEvent_t*>(ev), hipEventDisableTiming) == hipSuccess
+             ? KFAC_OK
+             : KFAC_ELAUNCH;
+}
+extern "C" int kfac_event_destroy(void* ev) {
+  return hipEventDestroy((hipEvent_t)ev) == hipSuccess ? KFAC_OK : KFAC_ELAUNCH;
+}
+extern "C" int kfac_event_record(void* ev, kfac_stream_t s) {
+  return hipEventRecord((hipEvent_t)ev, (hipStream_t)s) == hipSuccess ? KFAC_OK : KFAC_ELAUNCH;
+}
+extern "C" int kfac_stream_wait_event(kfac_stream_t s, void* ev) {
+  return hipStreamWaitEvent((hipStream_t)s, (hipEvent_t)ev, 0) == hipSuccess ? KFAC_OK : KFAC_ELAUNCH;
+}
+// 1: every work recorded before the event has completed, 0: not yet, < 0: error
+extern "C" int kfac_event_query(void* ev) {
+  const hipError_t e = hipEventQuery((hipEvent_t)ev);
+  return e == hipSuccess ? 1 : e == hipErrorNotReady ? 0 : KFAC_ELAUNCH;
+}
+extern "C" int kfac_event_synchronize(void* ev) {
+  return hipEventSynchronize((hipEvent_t)ev) == hipSuccess ? KFAC_OK : KFAC_ELAUNCH;
+}
+
 extern "C" int kfac_profile_reset(void) {
   std::lock_guard<std::mutex> lk(g_mu);
   for (const Rec& r : g_done) {

@@ -127,6 +127,29 @@ extern "C" int kfac_invert_ex(const kfac_invert_job* jobs, int njobs, void* work
   return KFAC_OK;
 }
 
+// The overlapped inversion's whole host sequence in one call (KFAC.invert beside the
+// next data pass): order `side` after `main`'s current work (event `order`), the grouped
+// inversion on `side` with `inputs_read` recorded after its F-reading launch, the pivot
+// verdict copied to pinned host memory, `done` recorded.  In Python the same sequence was
+// ~10 torch.cuda calls (stream / event objects, the stream context, a non-blocking
+// copy), ~100 us of the caller's thread per inversion on the bench host.
+extern "C" int kfac_invert_pipelined(const kfac_invert_job* jobs, int njobs, void* workspace,
+                                     size_t workspace_bytes, int32_t* info, int32_t* info_host,
+                                     void* order, void* inputs_read, void* done, kfac_stream_t main,
+                                     kfac_stream_t side) {
+  if (!info || !info_host || !order || !done || njobs <= 0) return KFAC_EINVAL;
+  if (hipEventRecord((hipEvent_t)order, (hipStream_t)main) != hipSuccess ||
+      hipStreamWaitEvent((hipStream_t)side, (hipEvent_t)order, 0) != hipSuccess)
+    return KFAC_ELAUNCH;
+  const int rc = kfac_invert_ex(jobs, njobs, workspace, workspace_bytes, info, inputs_read, side);
+  if (rc) return rc;
+  if (hipMemcpyAsync(info_host, info, (size_t)njobs * sizeof(int32_t), hipMemcpyDeviceToHost,
+                     (hipStream_t)side) != hipSuccess ||
+      hipEventRecord((hipEvent_t)done, (hipStream_t)side) != hipSuccess)
+    return KFAC_ELAUNCH;
+  return KFAC_OK;
+}
+
 extern "C" int kfac_invert(const kfac_invert_job* jobs, int njobs, void* workspace,
                            size_t workspace_bytes, int32_t* info, kfac_stream_t stream) {
   return kfac_invert_ex(jobs, njobs, workspace, workspace_bytes, info, nullptr, stream);

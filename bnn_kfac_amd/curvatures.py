@@ -266,7 +266,7 @@ class KFAC(Curvature):
             return
         ev = self._buf_read.pop(buf.data_ptr(), None)
         if ev is not None:
-            (stream or torch.cuda.current_stream(buf.device)).wait_event(ev)
+            self._wait(ev, stream, buf.device)
             self._pool_event(buf.device, ev)  # the wait captured its record: reusable
 
     def flush(self):
@@ -628,58 +628,68 @@ class KFAC(Curvature):
         # side stream starts after the work that produced `state`; the caller's
         # stream waits only until the factors have been READ (kfac_invert_ex's
         # inputs_read event, after the first launch), so it may overwrite them.
-        main = torch.cuda.current_stream(device)
+        # Host side (round 4): one kfac_invert_pipelined call orders the side stream after
+        # the caller's, runs the inversion, copies the verdict to pinned memory and
+        # records `done`, on raw HIP events (N.RawEvent): ~10 torch.cuda stream / event
+        # calls of 5-10 us each are gone from the caller's thread.  The L factors are
+        # allocated on the caller's stream: every use or release of them is ordered after
+        # `done` (_order_after), so the allocator's stream order covers the side stream.
+        main_h = N.stream_handle(device)
         latency_bound = max(F_.shape[0] for _, v in entries for F_ in v) <= 24 * 64
-        side = self._side_stream(device, alternate=latency_bound) if self.overlap_invert else main
-        read = None
-        if side is not main:
-            side.wait_stream(main)
-            read = self._event(device)
-            read.record(side)  # creates the event; kfac_invert_ex records it again
+        side = self._side_stream(device, alternate=latency_bound) if self.overlap_invert else None
+        side_h = side.cuda_stream if side is not None else main_h
         outs, jobs = [], []
-        with torch.cuda.stream(side):
-            for (layer, value), (n, s) in zip(entries, damping):
-                pair = []
-                for F_ in value:
-                    out = torch.empty_like(F_, memory_format=torch.contiguous_format)
-                    jobs.append(N.invert_job(F_, out, s ** 0.5, n ** 0.5))
-                    pair.append(out)
-                outs.append((layer, tuple(pair)))
-            info = N.invert(jobs, device, inputs_read=read)
-            # The pivot verdict travels back with a non-blocking copy into pinned
-            # memory, on the side stream; eager_verdict waits for it right here,
-            # otherwise it is settled at the next read of `inv_state` or the next
-            # invert(), so a data pass can be queued behind this inversion.
-            host = self._pinned_info(info)
-            host.copy_(info, non_blocking=True)
-            done = self._event(device)
-            done.record(side)
+        for (layer, value), (n, s) in zip(entries, damping):
+            pair = []
+            for F_ in value:
+                out = torch.empty_like(F_, memory_format=torch.contiguous_format)
+                jobs.append(N.invert_job(F_, out, s ** 0.5, n ** 0.5))
+                pair.append(out)
+            outs.append((layer, tuple(pair)))
+        read = self._event(device) if side is not None else None
+        done, order = self._event(device), self._event(device)
+        host = self._pinned_host(len(jobs))
+        N.invert_pipelined(jobs, device, host, order, read, done, main_h, side_h, side)
+        self._pool_event(device, order)  # (the side stream's wait captured its record)
         if read is not None:
-            self._release(main, read, entries)
+            self._release(main_h, read, entries, device)
         for layer, pair in outs:
             self._inv_state[layer] = pair
         self._inv_pending = _Pending(done, host, [layer for layer, _ in outs], self._inv_state,
-                                     [t for _, pair in outs for t in pair], side is not main)
+                                     [t for _, pair in outs for t in pair], side is not None)
         if self.eager_verdict:
             self._check_inverse()
 
     def _event(self, device):
-        """A torch.cuda.Event from the pool of settled ones (a verdict's `done` after
-        its host wait, an inputs-read event after the wait on it was enqueued)."""
+        """A raw HIP event (N.RawEvent) from the pool of settled ones (a verdict's `done`
+        after its host wait, an ordering event after the wait on it was enqueued)."""
         pool = self._event_pool.get(device.index)
-        return pool.pop() if pool else torch.cuda.Event()
+        return pool.pop() if pool else N.RawEvent()
 
     def _pool_event(self, device, ev):
         self._event_pool.setdefault(device.index, []).append(ev)
 
     def _pinned_info(self, info):
         """A pinned host int32 buffer for a verdict readback (pooled)."""
-        pool = self._info_pool
-        while pool and pool[-1].numel() != info.numel():
-            pool.pop()
-        return pool.pop() if pool else torch.empty(info.numel(), dtype=torch.int32, pin_memory=True)
+        return self._pinned_host(info.numel())
 
-    def _release(self, main, read, entries):
+    def _pinned_host(self, n):
+        pool = self._info_pool
+        while pool and pool[-1].numel() != n:
+            pool.pop()
+        return pool.pop() if pool else torch.empty(n, dtype=torch.int32, pin_memory=True)
+
+    @staticmethod
+    def _wait(ev, stream=None, device=None):
+        """Order `stream`'s (default: the current stream's) later work after `ev`
+        (a raw event or a torch.cuda.Event)."""
+        if isinstance(ev, N.RawEvent):
+            ev.wait_on(stream if isinstance(stream, int) else
+                       stream.cuda_stream if stream is not None else N.stream_handle(device))
+        else:
+            (stream if stream is not None else torch.cuda.current_stream(device)).wait_event(ev)
+
+    def _release(self, main_h, read, entries, device):
         """Let the caller's stream go past an inversion: straight away when the factors
         it reads are one of the double-buffered packed buffers (the buffer's next
         writer waits for `read` instead, see _await_readers), else behind `read`."""
@@ -689,8 +699,8 @@ class KFAC(Curvature):
             if all(F_.untyped_storage().data_ptr() == base for _, v in entries for F_ in v):
                 self._buf_read[buf.data_ptr()] = read
                 return
-        main.wait_event(read)
-        self._pool_event(main.device, read)
+        read.wait_on(main_h)
+        self._pool_event(device, read)
 
     def _side_stream(self, device, alternate=True):
         """The side stream of this inversion: two high-priority streams taken in turn,
@@ -711,15 +721,21 @@ class KFAC(Curvature):
         self._inv_turn = getattr(self, "_inv_turn", 0) ^ 1
         return s[self._inv_turn]
 
-    @staticmethod
-    def _order_after(pending):
-        """Later work on the caller's stream sees the inversion's factors, and the
-        allocator keeps their memory until that work has run (no host wait)."""
+    @classmethod
+    def _order_after(cls, pending):
+        """Later work on the caller's stream sees the inversion's factors (no host wait).
+        KFAC.invert allocates the factors on the caller's stream, so their release is
+        ordered after this wait too; factors allocated on another stream (the sharded
+        inversion's torch events) are also recorded on the caller's stream."""
         if pending.on_side:
-            cur = torch.cuda.current_stream(pending.outs[0].device)
-            cur.wait_event(pending.done)
-            for t in pending.outs:
-                t.record_stream(cur)
+            dev = pending.outs[0].device
+            if isinstance(pending.done, N.RawEvent):
+                pending.done.wait_on(N.stream_handle(dev))
+            else:
+                cur = torch.cuda.current_stream(dev)
+                cur.wait_event(pending.done)
+                for t in pending.outs:
+                    t.record_stream(cur)
 
     def _defer_verdict(self):
         """invert(): queue the pending inversion's verdict instead of waiting for it,
@@ -757,7 +773,7 @@ class KFAC(Curvature):
         pending.done.synchronize()
         bad = pending.host.numpy().copy()
         self._info_pool.append(pending.host)
-        if pending.outs:
+        if pending.outs and isinstance(pending.done, N.RawEvent):
             self._pool_event(pending.outs[0].device, pending.done)
         if bad.any():
             first = int(np.flatnonzero(bad)[0]) // 2  # two jobs (A, G) per layer

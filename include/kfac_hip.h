@@ -326,6 +326,25 @@ KFAC_API int kfac_profile_read(int id, double* total_ms, int64_t* launches);
 KFAC_API int kfac_profile_reset(void);
 
 /* ------------------------------------------------------------------- misc */
+/* KFAC.invert beside the next data pass (curvatures.py:367-398, overlapped), one call:
+ * record `order` on `main`, make `side` wait for it, run kfac_invert_ex on `side`
+ * (`inputs_read` recorded after the F-reading launch, may be NULL), copy the njobs
+ * verdicts from `info` (device) to `info_host` (pinned host memory) and record `done`
+ * on `side`.  Events come from kfac_event_create. */
+KFAC_API int kfac_invert_pipelined(const kfac_invert_job* jobs, int njobs, void* workspace,
+                                   size_t workspace_bytes, int32_t* info, int32_t* info_host,
+                                   void* order, void* inputs_read, void* done, kfac_stream_t main,
+                                   kfac_stream_t side);
+
+/* Raw HIP events for the host side's stream ordering (no reference counterpart: the
+ * reference is synchronous).  query: 1 complete, 0 pending, < 0 error. */
+KFAC_API int kfac_event_create(void** event);
+KFAC_API int kfac_event_destroy(void* event);
+KFAC_API int kfac_event_record(void* event, kfac_stream_t stream);
+KFAC_API int kfac_stream_wait_event(kfac_stream_t stream, void* event);
+KFAC_API int kfac_event_query(void* event);
+KFAC_API int kfac_event_synchronize(void* event);
+
 /* Release every HIP object the library keeps across calls (the inversion's cached
  * hipGraphs and their events, the profiling event pool), waiting for their last
  * use first.  Call before the HIP runtime shuts down (the Python binding registers

@@ -151,11 +151,39 @@ class _NoStream:
         return False
 
 
+class HostRawEvent:
+    """Test double of N.RawEvent (host work is synchronous: always complete)."""
+    def __init__(self):
+        self.handle = 0
+
+    def record(self, stream):
+        pass
+
+    def wait_on(self, stream):
+        pass
+
+    def query(self):
+        return True
+
+    def synchronize(self):
+        pass
+
+
+def fake_invert_pipelined(jobs, device, info_host, order, inputs_read, done, main, side, side_stream=None):
+    info = fake_invert(jobs, device)
+    info_host.copy_(info)
+    return info
+
+
 def install_cuda_stubs(kfac_list=()):
     """Stand-ins for the torch.cuda stream / event calls of KFAC.invert (run with
     overlap_invert False) so the plain single-device path runs on host memory; the
     verdict readback of each KFAC in `kfac_list` uses an unpinned buffer."""
     import torch
+    from bnn_kfac_amd import _native as N
+    N.RawEvent = HostRawEvent
+    N.invert_pipelined = fake_invert_pipelined
+    N.stream_handle = lambda device: 0
     stream = _HostStream()
     torch.cuda.current_stream = lambda device=None: stream
     torch.cuda.stream = _NoStream
@@ -163,6 +191,7 @@ def install_cuda_stubs(kfac_list=()):
     for k in kfac_list:
         k.overlap_invert = False
         k._pinned_info = lambda info: torch.empty(info.numel(), dtype=torch.int32)
+        k._pinned_host = lambda n: torch.empty(n, dtype=torch.int32)
 
 
 def install_distributed(kfac=None):

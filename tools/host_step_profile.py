@@ -56,6 +56,9 @@ def main():
     N.factor_accum_plan = lambda jobs: [(1, 256) for _ in jobs]
     N.require_device = lambda *a, **k: None
     N.invert = lambda jobs, device, inputs_read=None: torch.zeros(len(jobs), dtype=torch.int32)
+    N.invert_pipelined = lambda jobs, device, host, *a, **k: host.zero_()
+    N.RawEvent = host_double.HostRawEvent
+    N.stream_handle = lambda device: 0
     st = _St()
     torch.cuda.current_stream = lambda device=None: st
     torch.cuda.Stream = lambda *a, **k: _St()
@@ -69,6 +72,7 @@ def main():
     kfac.eager_verdict = False
     kfac.launch_first = 16
     kfac._pinned_info = lambda info: torch.empty(info.numel(), dtype=torch.int32)
+    kfac._pinned_host = lambda n: torch.empty(n, dtype=torch.int32)
     for t in (torch.Tensor.record_stream,):
         pass
     torch.Tensor.record_stream = lambda self, s: None
