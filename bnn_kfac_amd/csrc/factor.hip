@@ -48,6 +48,11 @@ struct FactorArgs {
   int split_major;  // LDS-DMA path task order: 1 split-major, 0 tile-major (KFAC_SYRK_ORDER)
   int task_end[MAXJ];
   int tile_end[MAXJ];
+  // kfac_factor_tiles_x3, jobs of equal splits: the tasks of ONE split of every job
+  // are contiguous (unit_end: prefix sums of the jobs' units), so xcd_task hands each
+  // XCD whole K-ranges of all factors (KFAC_X3_INTERLEAVE)
+  int interleave;
+  int unit_end[MAXJ];
   FactorJobDev job[MAXJ];
 };
 
@@ -811,6 +816,9 @@ __device__ __forceinline__ X3Frag x3_split8(const float (&x)[8]) {
 // the buffer's record limit (0), and the ones column (FILL: only the tasks whose
 // fragments hold it) is a select of 1 / 0 by row validity.
 // Microbench: tools/microbench/x3w_mb.hip; DESIGN.md §3.1c.
+#ifndef KFAC_X3_AB_FULL
+#define KFAC_X3_AB_FULL 0
+#endif
 #ifndef KFAC_X3_AB
 #define KFAC_X3_AB 0  // timing A/B builds (tools/build_ab.sh): 1 no reloads, 2 no split, 3 neither
 #endif
@@ -1181,6 +1189,19 @@ __device__ __forceinline__ void x3_loop_dma(const FactorJobDev& J, const float* 
   vm_wait(0);  // (the ring's last pieces land before the epilogue reuses the LDS)
 }
 
+#ifndef KFAC_X3_STAMPS
+#define KFAC_X3_STAMPS 0  // diagnostic builds only: per-workgroup timeline of the x3 launch
+#endif
+#if KFAC_X3_STAMPS
+// [block][8]: realtime at start / loop start / loop end / end, shader clocks at loop
+// start / end, HW_ID, XCC_ID | mask << 8 | stages << 16 (tools/x3_stamps.py)
+__device__ unsigned long long g_x3_stamps[8192 * 8];
+#define X3_STAMP(i, v) \
+  if (threadIdx.x == 0 && blockIdx.x < 8192) g_x3_stamps[blockIdx.x * 8 + (i)] = (unsigned long long)(v)
+#else
+#define X3_STAMP(i, v)
+#endif
+
 template <int GBK, int NSLOT>
 __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const float* const* segs, int local,
                                                float* lds, int split_major) {
@@ -1204,6 +1225,9 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
       act[bi][bj] = !(same && bi < bj) && ti * TILE + bi * 32 < J.n && tj * TILE + bj * 32 < J.n;
       mask |= act[bi][bj] << (2 * bi + bj);
     }
+#if KFAC_X3_AB_FULL  // timing A/B only: every tile runs the full-tile loop (balance probe)
+  mask = 15;
+#endif
   floatx16 acc[2][2];
 #pragma unroll
   for (int bi = 0; bi < 2; ++bi)
@@ -1211,6 +1235,9 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
     for (int bj = 0; bj < 2; ++bj)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[bi][bj][v] = 0.f;
+  X3_STAMP(1, wall_clock64());
+  X3_STAMP(4, __builtin_amdgcn_s_memtime());
+  X3_STAMP(7, (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) | (mask << 8) | ((uint32_t)(s1 - s0) << 16));
   if (s1 > s0) {
     // FILL: one of the task's fragments holds the ones column (the last tile row /
     // column of an A factor with a bias)
@@ -1235,6 +1262,8 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
     }
 #undef X3_CASE
   }
+  X3_STAMP(2, wall_clock64());
+  X3_STAMP(5, __builtin_amdgcn_s_memtime());
   // wave w stores block row w: it hands the other block row's partials to the other
   // wave through LDS (the ring is free after the barrier), then adds the other
   // wave's.  Both sums are w0 + w1 (IEEE addition commutes): deterministic.
@@ -1273,17 +1302,34 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
 __global__ __launch_bounds__(X3_THREADS, 2) void kfac_factor_tiles_x3(FactorArgs args) {
   // (the epilogue's hand-off of a block row, 16 KB; KFAC_X3_DMA: the waves' rings, 32 KB)
   __shared__ __attribute__((aligned(16))) float lds[KFAC_X3_DMA ? 4 * X3D_SLOT : 2 * BK * TILE];
+  X3_STAMP(0, wall_clock64());
+  X3_STAMP(6, (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4));
   for (int i = 0; i < args.stagger * (int)(blockIdx.x >> 8); ++i) __builtin_amdgcn_s_sleep(8);
   const int task = xcd_task(blockIdx.x, gridDim.x);
-  int j = 0;
-  while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
+  int j = 0, local;
+  if (args.interleave) {  // task = split * U + unit of the concatenated jobs' units
+    const int U = args.unit_end[args.njobs - 1];
+    const int sp = task / U, u = task - sp * U;
+    while (j + 1 < args.njobs && u >= args.unit_end[j]) ++j;
+    const int ub = j ? args.unit_end[j - 1] : 0;
+    local = sp * (args.unit_end[j] - ub) + (u - ub);  // (split-major local order)
+  } else {
+    while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
+    local = task - args.job[j].task_begin;
+  }
   const FactorJobDev& J = args.job[j];
-  const int local = task - J.task_begin;
   if (J.n <= 32)
     factor_task_narrow_direct<X3_NW>(J, args.segs, local, lds);
   else
     factor_task_x3<BK, 2>(J, args.segs, local, lds, args.split_major);
+  X3_STAMP(3, wall_clock64());
 }
+
+#if KFAC_X3_STAMPS
+extern "C" __attribute__((visibility("default"))) int kfac_debug_x3_stamps(void* host, size_t bytes) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_x3_stamps), std::min(bytes, sizeof(g_x3_stamps))) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // ------------------------------------------------------------ conv operands
 // Conv2d factors with each image staged whole in LDS (replaces the per-element
@@ -2105,6 +2151,11 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
       continue;
     }
     p.splits = (int)cdiv(steps, best_c);
+    static const int forced_splits = [] {  // (tuning experiments: KFAC_SYRK_SPLITS)
+      const char* v = getenv("KFAC_SYRK_SPLITS");
+      return v ? atoi(v) : 0;
+    }();
+    if (forced_splits > 0) p.splits = (int)std::min<int64_t>(forced_splits, steps);
     ConvGeom cg;
     if (conv_geom(jobs[i], cg)) {
       // Tasks own whole images, the SAME number k each, and fill the resident slots
@@ -2231,6 +2282,20 @@ static int prepare_group(const kfac_factor_job* jobs, int njobs, char* ws, size_
   g.tasks = tasks;
   g.rtiles = rtiles;
   g.split_tasks = 0;
+  {
+    static const int inter = [] {
+      const char* e = getenv("KFAC_X3_INTERLEAVE");
+      return e ? atoi(e) : 0;
+    }();
+    bool same = inter && args.split_major;
+    int u = 0;
+    for (int i = 0; i < njobs && same; ++i) {
+      same = plans[i].splits == plans[0].splits && plans[i].tasks == plans[i].units * plans[i].splits;
+      u += plans[i].units;
+      args.unit_end[i] = u;
+    }
+    args.interleave = same;  // (read by kfac_factor_tiles_x3 only)
+  }
   if (syrk3_group(jobs, njobs)) {
     // the pre-split images after the slabs; the split launch's own task ranges
     g.split = args;

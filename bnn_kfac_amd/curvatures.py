@@ -147,6 +147,11 @@ class Curvature(ABC):
         print('Loading %s complete!\n' % filename)
 
 
+def _same_shapes(f, g):
+    """Two fast-path templates of the same record signature (layers, shapes, strides)."""
+    return all(a[:7] == b[:7] for a, b in zip(f[1], g[1])) and len(f[1]) == len(g[1])
+
+
 class _Pending(NamedTuple):
     """An inversion whose pivot verdict is not read yet."""
     done: Any            # torch.cuda.Event after the verdict's copy to `host`
@@ -225,6 +230,8 @@ class KFAC(Curvature):
         # pass is no longer overlapped): kept at 1.
         self.launch_first = 1    # (property: also restarts the doubling)
         self._fast = None        # job templates of the last slow-path update (see _remember)
+        self._fast_alt = []      # this cycle's other valid templates (other batch shapes)
+        self._fast_cache = {}    # packed buffer data_ptr -> templates onto its views (cycle starts)
         self._acc_buf = None     # device buffer of the accumulators
         self._acc_map = None     # F pointer -> (acc pointer, splits) of the pending cycle
         self._acc_live = set()   # F pointers already written in the pending cycle
@@ -249,6 +256,7 @@ class KFAC(Curvature):
         self._queue_bytes = 0
         self._launch_at = self.launch_first
         self._fast = None
+        self._fast_alt = []
         self._acc_flush = self._acc_map = None
         self._state = dict()
         self.inv_state = dict()
@@ -403,12 +411,21 @@ class KFAC(Curvature):
     def update(self, batch_size: int):
         """Accumulate this batch's factors for every selected layer
         (curvatures.py:325-365; `batch_size` is unused there too)."""
-        fast = self._fast
-        if fast is not None and self.defer_reduce:
-            entry = self._fast_entry(fast)
-            if entry is not None:
-                self._enqueue(entry)
-                return
+        if self.defer_reduce:
+            fast = self._fast
+            if fast is not None:
+                entry = self._fast_entry(fast)
+                if entry is None and self._fast_alt:
+                    entry = self._fast_other()
+                if entry is not None:
+                    self._enqueue(entry)
+                    return
+            elif not self._state and self._packed is not None:
+                entry = self._fast_begin()
+                if entry is not None:
+                    self._enqueue(entry)
+                    return
+        cycle_start = not self._state
         prepared = []
         for layer in self._layers():
             forward, backward = self.record[layer]
@@ -431,12 +448,12 @@ class KFAC(Curvature):
             self._await_readers()
             N.factor_update(jobs, device)
             return
-        self._remember(prepared, jobs, device)
+        self._remember(prepared, jobs, device, cycle_start)
         # merge key: the fast path's job templates when later updates can reuse them
         # (they differ from `jobs` only in beta and pointers), else this update alone
         key = self._fast[2] if self._fast is not None else tuple(jobs)
         self._enqueue((tuple(jobs), tuple(j.x.ptr for j in jobs), keep,
-                       [t._version for t in keep], device, key))
+                       [t._version for t in keep], device, key, None))
 
     # Fast path: a later update whose records have the same shapes, strides, dtype and
     # device as the last slow-path one, and whose targets are still the same `state`
@@ -446,7 +463,8 @@ class KFAC(Curvature):
     def _signature(t):
         return t.shape, t.stride(), t.dtype, t.device
 
-    def _remember(self, prepared, jobs, device):
+    def _remember(self, prepared, jobs, device, cycle_start=False):
+        old = self._fast
         self._fast = None
         spec = []
         for layer, _opA, _opG, _nA, _nG, kept in prepared:
@@ -460,18 +478,33 @@ class KFAC(Curvature):
             # field, cheapest first; the signature of _signature, unpacked)
             spec.append((layer, forward.shape, backward.shape, forward.stride(), backward.stride(),
                          forward.dtype, forward.get_device(), lst, lst[0], lst[1]))
-        tmpl = []
+        tmpl, tmpl0 = [], []
         for j in jobs:
             t = N.FactorJob.from_buffer_copy(j)
             t.beta = 1.0
             tmpl.append(t)
-        self._fast = (getattr(self, "_scale", 1.0), spec, tuple(tmpl), device)
+            t = N.FactorJob.from_buffer_copy(j)
+            t.beta = 0.0
+            tmpl0.append(t)
         # bytes of the records one fast-path update keeps queued (the signatures fix them)
-        self._fast_bytes = sum(t.numel() * t.element_size()
-                               for layer, *_ in prepared for t in self.record[layer])
+        nbytes = sum(t.numel() * t.element_size() for layer, *_ in prepared for t in self.record[layer])
+        fast = self._fast = (getattr(self, "_scale", 1.0), spec, tuple(tmpl), device, tuple(tmpl0), nbytes)
+        # the templates of other batch shapes stay usable this cycle (same state lists)
+        if old is not None and old[1][0][7] is spec[0][7]:
+            self._fast_alt = [f for f in [old] + self._fast_alt if not _same_shapes(f, fast)][:3]
+        # templates onto this packed buffer's own views start later cycles on it
+        # (_fast_begin); kept per buffer, one per batch shape, the cycle's first update
+        # shape first
+        views = self._packed_views
+        buf = self._packed
+        if buf is not None and all(views.get(e[0], (None, None))[0] is e[8] and views[e[0]][1] is e[9]
+                                   for e in spec):
+            lst = [f for f in self._fast_cache.get(buf.data_ptr(), []) if not _same_shapes(f, fast)]
+            lst.insert(0 if cycle_start else len(lst), fast)
+            self._fast_cache[buf.data_ptr()] = lst[:4]
 
-    def _fast_entry(self, fast):
-        scale, spec, tmpl, device = fast
+    def _fast_entry(self, fast, begin=False):
+        scale, spec, tmpl, device, tmpl0, nbytes = fast
         if getattr(self, "_scale", 1.0) != scale:
             return None
         record, state = self.record, self._state
@@ -484,12 +517,53 @@ class KFAC(Curvature):
                     or backward.dtype != dtype or forward.stride() != str_f or backward.stride() != str_b
                     or forward.get_device() != dev or backward.get_device() != dev):
                 return None
-            if state.get(layer) is not lst or lst[0] is not A or lst[1] is not G:
+            if begin:
+                v = self._packed_views.get(layer)
+                if v is None or v[0] is not A or v[1] is not G:
+                    return None
+            elif state.get(layer) is not lst or lst[0] is not A or lst[1] is not G:
                 return None
             ptrs += (forward.data_ptr(), backward.data_ptr())
             keep += (forward, backward)
             versions += (forward._version, backward._version)
-        return tmpl, tuple(ptrs), keep, versions, device, tmpl
+        return tmpl0 if begin else tmpl, tuple(ptrs), keep, versions, device, tmpl, nbytes
+
+    def _fast_other(self):
+        """An update of another batch shape seen this cycle (the pass's short last
+        batch): its template becomes the primary one."""
+        for i, f in enumerate(self._fast_alt):
+            entry = self._fast_entry(f)
+            if entry is not None:
+                self._fast_alt[i] = self._fast
+                self._fast = f
+                return entry
+        return None
+
+    def _fast_begin(self):
+        """The first update of a cycle (empty state, after reset()) on a packed buffer a
+        slow-path update already wrote: a cached template onto the buffer's views whose
+        record signature matches creates the state entries (as _target does) and queues
+        the update with the template's beta-0 jobs; the buffer's other templates are
+        re-bound to the new state lists for the rest of the cycle."""
+        cached = self._fast_cache.get(self._packed.data_ptr())
+        if not cached:
+            return None
+        for i, f in enumerate(cached):
+            entry = self._fast_entry(f, begin=True)
+            if entry is None:
+                continue
+            state = self._state
+            lists = {}
+            for e in f[1]:
+                lists[e[0]] = state[e[0]] = [e[8], e[9]]
+            rebound = []
+            for g in [f] + cached[:i] + cached[i + 1:]:
+                spec = [e[:7] + (lists[e[0]], e[8], e[9]) if e[0] in lists else e for e in g[1]]
+                rebound.append(g[:1] + (spec,) + g[2:])
+            self._fast, self._fast_alt = rebound[0], rebound[1:]
+            cached[:] = rebound
+            return entry
+        return None
 
     def _enqueue(self, entry):
         """Queue one update: (jobs, operand pointers, records kept alive, their
@@ -498,8 +572,8 @@ class KFAC(Curvature):
         if queue and queue[0][4] is not entry[4] and queue[0][4] != entry[4]:
             self._launch_queue()
         self._queue.append(entry)
-        fast = self._fast
-        self._queue_bytes += (self._fast_bytes if fast is not None and entry[0] is fast[2]
+        nbytes = entry[6]
+        self._queue_bytes += (nbytes if nbytes is not None
                               else sum(t.numel() * t.element_size() for t in entry[2]))
         # launch sizes double from `launch_first` up to defer_batches (the records held
         # are capped by defer_bytes): a function of the update count only, so the
@@ -517,7 +591,7 @@ class KFAC(Curvature):
         walks the batches; Conv2d im2col / channel-major: the images walk them)."""
         queue, self._queue = self._queue, []
         self._queue_bytes = 0
-        for _jobs, _ptrs, keep, versions, _dev, _key in queue:
+        for _jobs, _ptrs, keep, versions, _dev, _key, _nbytes in queue:
             for t, v in zip(keep, versions):
                 if t._version != v:
                     raise RuntimeError(

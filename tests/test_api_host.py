@@ -213,6 +213,55 @@ def test_queued_updates_merge_into_multibatch_jobs(monkeypatch):
         np.testing.assert_allclose(g, w, rtol=1e-6)
 
 
+def test_fast_path_across_cycles(monkeypatch):
+    """Passes of full batches and a short last one, reset() between them (the bench's
+    loop, double-buffered packed state): after one pass per packed buffer, no update
+    takes the slow path any more -- the cycle's first update starts from the buffer's
+    cached template (beta 0, state entries re-created), the short batch from this
+    cycle's alternate template -- and every pass's factors equal the immediate path's."""
+    from bnn_kfac_amd.curvatures import KFAC
+    host_double.install(monkeypatch)
+    rng = np.random.default_rng(11)
+    sizes = (8, 8, 8, 5)
+    batches = [[torch.tensor(rng.random((B, 6), dtype=np.float32)),
+                torch.tensor(rng.standard_normal((B, 5)).astype(np.float32)),
+                torch.tensor(rng.random((B, 5), dtype=np.float32)),
+                torch.tensor(rng.standard_normal((B, 3)).astype(np.float32))]
+               for B in sizes]
+    net = mlp()
+    ref = KFAC(net)
+    ref.defer_reduce = False
+    for a1, g1, a2, g2 in batches:
+        ref.record[net[0]], ref.record[net[2]] = [a1, g1], [a2, g2]
+        ref.update(a1.shape[0])
+    want = [t.clone().numpy() for pair in ref.state.values() for t in pair]
+    kfac = KFAC(net)
+    kfac.launch_first = 16
+    slow = []
+    orig = KFAC._remember
+    monkeypatch.setattr(KFAC, "_remember", lambda self, *a, **k: (slow.append(1), orig(self, *a, **k))[1])
+    per_pass = []
+    for p in range(5):
+        kfac.reset()
+        n0 = len(slow)
+        for a1, g1, a2, g2 in batches:
+            kfac.record[net[0]], kfac.record[net[2]] = [a1, g1], [a2, g2]
+            kfac.update(a1.shape[0])
+        per_pass.append(len(slow) - n0)
+        got = [t.clone().numpy() for pair in kfac.state.values() for t in pair]
+        assert list(kfac.state) == [net[0], net[2]]  # modules() order
+        for g, w in zip(got, want):
+            np.testing.assert_allclose(g, w, rtol=1e-6)
+    assert per_pass == [2, 2, 0, 0, 0]
+    # a record of a new shape still takes the slow path (and is cached from then on)
+    kfac.reset()
+    a1, g1, a2, g2 = [t[:3] for t in batches[0]]
+    kfac.record[net[0]], kfac.record[net[2]] = [a1, g1], [a2, g2]
+    n0 = len(slow)
+    kfac.update(3)
+    assert len(slow) == n0 + 1
+
+
 def test_queued_record_modified_in_place_raises(monkeypatch):
     from bnn_kfac_amd.curvatures import KFAC
     host_double.install(monkeypatch)
