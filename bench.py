@@ -400,6 +400,8 @@ def main(argv=None):
     ap.add_argument("--launch-first", type=int, default=None,
                     help="queued updates in a pass's first SYRK launch (KFAC.launch_first) for both "
                          "loops (default: 16 for the pipelined loop, the library's 1 for the serial one)")
+    ap.add_argument("--max-pending", type=int, default=None,
+                    help="KFAC.max_pending: inversions with an unread verdict before invert() waits (A/B)")
     ap.add_argument("--defer-mb", type=int, default=None,
                     help="KFAC.defer_bytes in MiB (records a queued launch may hold; A/B)")
     ap.add_argument("--single-buffer", action="store_true",
@@ -473,6 +475,8 @@ def main(argv=None):
         kfac.double_buffer = False
     if args.defer_mb:
         kfac.defer_bytes = args.defer_mb << 20
+    if args.max_pending:
+        kfac.max_pending = args.max_pending
     recs = synthetic_records(specs, images, device, seed=1234 + rank)
     starts = list(range(0, images, batch))
     comm = {"ms": 0.0, "n": 0, "timing": False}

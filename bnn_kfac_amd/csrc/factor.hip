@@ -1005,190 +1005,6 @@ __device__ __forceinline__ void x3_loop(const FactorJobDev& J, const float* cons
   }
 }
 
-// The same stage schedule with the operand panels brought in by LDS-DMA
-// (buffer_load_dwordx4 ... lds: 16 bytes a lane, 1 KB an instruction) into a ring of
-// two 16-row slots PER WAVE (no barrier: a wave reads only the rows it brought in),
-// issued two stages ahead; fragments are gathered with ds_read_b32 (one 32-lane half
-// per row, conflict-free) one segment before their split.  Per wave and stage: 8 DMA
-// instructions (4 on a diagonal tile) instead of 32 dword loads (the texture-address
-// path's instruction count / 4) and no register holds a load in flight.
-// Slot image: [16 rows][A panel 64 | B panel 64] floats (diagonal tiles: A only).
-#ifndef KFAC_X3_DMA
-#define KFAC_X3_DMA 0
-#endif
-constexpr int X3D_SLOT = 16 * 2 * TILE;  // floats per wave slot
-
-template <int NV>
-__device__ __forceinline__ void x3d_pattern() {  // 6 MFMAs, NV VALU each, the DS reads early
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);               // MFMA
-    if (NV > 0) __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);  // VALU
-    if (i < 4) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);    // DS read
-  }
-}
-
-template <int MASK, bool FILL>
-__device__ __forceinline__ void x3_loop_dma(const FactorJobDev& J, const float* const* segs, int ti, int tj,
-                                            int64_t s0, int64_t s1, floatx16 (&acc)[2][2], float* lds) {
-  constexpr bool A00 = MASK & 1;
-  constexpr bool SAME = MASK == 13 || MASK == 1;
-  static_assert(A00, "block (0, 0) always has work");
-  constexpr int PW = SAME ? TILE : 2 * TILE;  // slot row width (floats)
-  constexpr int NI = 16 * PW / 256;           // DMA instructions per wave and stage
-  constexpr int LPR = PW / 4;                 // lanes per slot row
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int ld4 = (int)J.x.ld * 4;
-  const int rows = (int)J.x.rows;
-  const int rec = rows * ld4;
-  float* wl = lds + wave * 2 * X3D_SLOT;  // this wave's two slots
-  // DMA lane: row lane / LPR of the instruction's 1024 / (4 PW) rows, 4 columns
-  int dvo;
-  {
-    const int pc = (lane % LPR) * 4;  // slot column
-    const int c = (pc < TILE ? ti * TILE + pc : tj * TILE + pc - TILE);
-    dvo = c < J.x.cols ? (lane / LPR) * ld4 + c * 4 : rec;
-  }
-  const int lr = 8 * (lane >> 5);  // the lane's first row within its wave's 16
-  bool onesl[4];
-#pragma unroll
-  for (int f = 0; f < 4; ++f) onesl[f] = (f < 2 ? ti : tj) * TILE + (f & 1) * 32 + (lane & 31) == J.x.ones;
-  const int ns = (int)(s1 - s0);
-  const int lastseg = J.nseg - 1;
-  X3Cursor c2;
-  c2.seg = (int)(s0 / J.sps);
-  c2.k = (int)((s0 - (int64_t)c2.seg * J.sps) * BK);
-  c2.b = seg_base(J, segs, c2.seg);
-  const float* nb = seg_base(J, segs, min(c2.seg + 1, lastseg));
-  int left = ns - 1;
-  auto advance = [&](X3Cursor& c) {
-    const bool more = left > 0;
-    const bool wrap = more && c.k + BK >= rows;
-    c.k = more ? (wrap ? 0 : c.k + BK) : c.k;
-    c.seg += wrap;
-    c.b = wrap ? nb : c.b;
-    nb = seg_base(J, segs, min(c.seg + 1, lastseg));
-    left -= more;
-  };
-  // DMA the wave's 16 rows of cursor c's stage into slot sl; returns the stage's first row
-  auto dma = [&](X3Cursor& c, float* sl) {
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(c.b), 0, rec, 0x00020000);
-    const int sb = (c.k + 16 * wave) * ld4;
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, sl + i * 256, 16, dvo, sb + i * (1024 / (4 * PW)) * ld4, 0, 0);
-    const int k = c.k;
-    advance(c);
-    return k;
-  };
-  const int rd0 = lr * PW + (lane & 31);
-  auto rd = [&](int f, const float* sl, float (&x)[8]) {  // fragment f's 8 rows from slot sl
-    const float* p = sl + rd0 + ((SAME ? 0 : (f >> 1) * TILE) + (f & 1) * 32);
-#pragma unroll
-    for (int r = 0; r < 8; ++r) x[r] = p[r * PW];
-  };
-  auto sp = [&](int f, int kstage, float (&x)[8]) {
-    if constexpr (FILL) {
-      const int nvalid = rows - kstage - 16 * wave;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) x[r] = onesl[f] ? (lr + r < nvalid ? 1.f : 0.f) : x[r];
-    }
-    return x3_split8(x);
-  };
-  auto slot = [&](int st) { return wl + (st & 1) * X3D_SLOT; };
-  // prologue: stages s0, s0 + 1 in flight; the first block's fragments split
-  int kc = dma(c2, slot(0));
-  int kn = dma(c2, slot(1));
-  vm_wait(NI);
-  float xr[8], xq[8];
-  rd(0, slot(0), xr);
-  X3Frag pa = sp(0, kc, xr), pb = pa;
-  if constexpr (!SAME) {
-    rd(2, slot(0), xr);
-    pb = sp(2, kc, xr);
-  }
-  if constexpr (MASK == 15 || MASK == 13 || MASK == 5) rd(1, slot(0), xr);
-  else if constexpr (MASK == 3) rd(3, slot(0), xr);
-  constexpr int NV = FILL ? 52 / 6 + 1 : 44 / 6 + 1;
-  // the slot of stage st is refilled with stage st + 2 once its last fragment is read
-  for (int st = 0; st < ns; ++st) {
-    float* cur = slot(st);
-    float* nxt = slot(st + 1);
-    X3Frag qa, qb;
-    int knn;
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (MASK == 15) {
-      const X3Frag A1 = sp(1, kc, xr);
-      rd(3, cur, xr);
-      x3_six(acc[0][0], pa, pb);
-      x3d_pattern<NV>();
-      __builtin_amdgcn_sched_barrier(0);
-      const X3Frag B1 = sp(3, kc, xr);
-      knn = dma(c2, cur);
-      vm_wait(NI);  // stage st + 1 landed
-      rd(0, nxt, xr);
-      x3_six(acc[1][0], A1, pb);
-      x3d_pattern<NV>();
-      __builtin_amdgcn_sched_barrier(0);
-      qa = sp(0, kn, xr);
-      rd(2, nxt, xr);
-      x3_six(acc[0][1], pa, B1);
-      x3d_pattern<NV>();
-      __builtin_amdgcn_sched_barrier(0);
-      qb = sp(2, kn, xr);
-      rd(1, nxt, xr);
-      x3_six(acc[1][1], A1, B1);
-      x3d_pattern<NV>();
-    } else if constexpr (MASK == 13) {
-      const X3Frag A1 = sp(1, kc, xr);
-      knn = dma(c2, cur);
-      vm_wait(NI);
-      rd(0, nxt, xr);
-      x3_six(acc[0][0], pa, pa);
-      x3d_pattern<NV>();
-      __builtin_amdgcn_sched_barrier(0);
-      qa = sp(0, kn, xr);
-      rd(1, nxt, xr);
-      x3_six(acc[1][0], A1, pa);
-      x3d_pattern<NV>();
-      __builtin_amdgcn_sched_barrier(0);
-      x3_six(acc[1][1], A1, A1);
-      x3d_pattern<0>();
-      qb = qa;
-    } else if constexpr (MASK == 5 || MASK == 3) {
-      constexpr int F1 = MASK == 5 ? 1 : 3;
-      const X3Frag X1 = sp(F1, kc, xr);
-      knn = dma(c2, cur);
-      vm_wait(NI);
-      rd(0, nxt, xr);
-      rd(2, nxt, xq);
-      x3_six(acc[0][0], pa, pb);
-      x3d_pattern<NV>();
-      __builtin_amdgcn_sched_barrier(0);
-      qa = sp(0, kn, xr);
-      qb = sp(2, kn, xq);
-      rd(F1, nxt, xr);
-      if constexpr (MASK == 5) x3_six(acc[1][0], X1, pb);
-      else x3_six(acc[0][1], pa, X1);
-      x3d_pattern<2 * NV>();
-    } else {  // 1
-      knn = dma(c2, cur);
-      vm_wait(NI);
-      rd(0, nxt, xr);
-      qa = sp(0, kn, xr);
-      x3_six(acc[0][0], pa, pa);
-      x3d_pattern<NV>();
-      qb = qa;
-    }
-    pa = qa;
-    pb = qb;
-    kc = kn;
-    kn = knn;
-  }
-  vm_wait(0);  // (the ring's last pieces land before the epilogue reuses the LDS)
-}
-
 #ifndef KFAC_X3_STAMPS
 #define KFAC_X3_STAMPS 0  // diagnostic builds only: per-workgroup timeline of the x3 launch
 #endif
@@ -1244,13 +1060,8 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
     const bool fill = J.x.ones >= 0 && ((J.x.ones >> 6) == ti || (J.x.ones >> 6) == tj);
 #define X3_CASE(M)                                                   \
   case M:                                                            \
-    if constexpr (KFAC_X3_DMA) {                                     \
-      if (fill) x3_loop_dma<M, true>(J, segs, ti, tj, s0, s1, acc, lds); \
-      else x3_loop_dma<M, false>(J, segs, ti, tj, s0, s1, acc, lds);     \
-    } else {                                                         \
-      if (fill) x3_loop<M, true>(J, segs, ti, tj, s0, s1, acc);      \
-      else x3_loop<M, false>(J, segs, ti, tj, s0, s1, acc);          \
-    }                                                                \
+    if (fill) x3_loop<M, true>(J, segs, ti, tj, s0, s1, acc);        \
+    else x3_loop<M, false>(J, segs, ti, tj, s0, s1, acc);            \
     break;
     switch (mask) {  // (block (0, 0) always has work)
       X3_CASE(15)
@@ -1300,8 +1111,8 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
 // 2 waves per SIMD (178 VGPRs): 4 workgroups per CU leave a 32-tile inversion
 // workgroup (107 registers, 29 KB) room to run beside the pass
 __global__ __launch_bounds__(X3_THREADS, 2) void kfac_factor_tiles_x3(FactorArgs args) {
-  // (the epilogue's hand-off of a block row, 16 KB; KFAC_X3_DMA: the waves' rings, 32 KB)
-  __shared__ __attribute__((aligned(16))) float lds[KFAC_X3_DMA ? 4 * X3D_SLOT : 2 * BK * TILE];
+  // (LDS only for the epilogue's hand-off of a block row, 16 KB)
+  __shared__ __attribute__((aligned(16))) float lds[2 * BK * TILE];
   X3_STAMP(0, wall_clock64());
   X3_STAMP(6, (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4));
   for (int i = 0; i < args.stagger * (int)(blockIdx.x >> 8); ++i) __builtin_amdgcn_s_sleep(8);
@@ -2102,7 +1913,11 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
   const bool s3 = syrk3_group(jobs, njobs);
   // resident workgroups per CU: 4 (32 KB of LDS each; kfac_factor_tiles_x3: 4 of two
   // waves -- 3 or 2 measured slower); the bf16x3 kernel: S3D_WGS (49 KB each)
-  if (slots <= 0) slots = (s3 ? S3D_WGS : 4) * 256;
+  static const int env_wgs = [] {  // (tuning experiments: resident workgroups per CU planned for)
+    const char* v = getenv("KFAC_SYRK_WGS");
+    return v ? atoi(v) : 0;
+  }();
+  if (slots <= 0) slots = (env_wgs > 0 ? env_wgs : (s3 ? S3D_WGS : 4)) * 256;
   constexpr int64_t MIN_CHUNK = 8, OVERHEAD = 4;  // stages; ~per-task fixed cost in stages
   int64_t max_steps = 1;
   for (int i = 0; i < njobs; ++i) max_steps = std::max(max_steps, job_stages(jobs[i]));

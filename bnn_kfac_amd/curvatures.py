@@ -248,6 +248,9 @@ class KFAC(Curvature):
         # the next inv_state read or invert(), so the next data pass is queued behind
         # the inversion without a host sync and overlaps it.
         self.eager_verdict = True
+        # eager_verdict False: inversions whose verdict may stay unread (and whose
+        # factors stay queued) before invert() waits for the oldest one
+        self.max_pending = 2
         self._inv_streams = {}    # device index -> side streams
 
     def reset(self):
@@ -813,14 +816,14 @@ class KFAC(Curvature):
 
     def _defer_verdict(self):
         """invert(): queue the pending inversion's verdict instead of waiting for it,
-        and read the verdicts that are already back (at most 2 stay queued).  Queued
+        and read the verdicts that are already back (at most `max_pending` stay queued).  Queued
         inversions are ordered before the caller's stream only when `inv_state` is
         read (_check_inverse), so the next data pass does not wait for them."""
         pending = getattr(self, "_inv_pending", None)
         if pending is not None:
             self._inv_pending = None
             self._inv_older.append(pending)
-        while self._inv_older and (len(self._inv_older) > 2 or self._inv_older[0].done.query()):
+        while self._inv_older and (len(self._inv_older) > self.max_pending or self._inv_older[0].done.query()):
             p = self._inv_older.pop(0)
             self._order_after(p)
             self._verdict(p)

@@ -15,7 +15,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
 rc=$?; echo "trace rc=$rc"; ok $rc || exit $rc
 timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1
 for C in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" \
-         "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM"; do
+         "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM" "TCC_HIT_sum TCC_MISS_sum"; do
   name=$(echo $C | tr ' ' '_')
   timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "kfac_factor|inv_|kfac_quad" --output-format csv \
       -d $OUT/pmc_$name -o run -- $BENCH > $OUT/pmc_$name.log 2>&1

@@ -23,3 +23,10 @@ for f in sorted(glob.glob("gpurun_out/r04m/pmc_*/run_counter_collection.csv")):
         s[r["Counter_Name"]] += float(r["Counter_Value"]); d[r["Counter_Name"]].add(r["Dispatch_Id"])
     print(f.split("/")[2], {k: round(v / len(d[k])) for k, v in s.items()})
 PY
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-e2e --no-serial > $O/trace_bench.log 2>&1 || { echo "trace rc=$?"; tail -5 $O/trace_bench.log; exit 1; }
+python tools/trace_gaps.py $(ls $O/trace/*kernel_trace.csv | head -1) 3.0 > $O/trace_gaps.txt 2>&1 || { cat $O/trace_gaps.txt; exit 1; }
+cat $O/trace_gaps.txt
+for lf in 4 8; do
+  timeout -k 10 300 python bench.py --no-cpu-baseline --no-e2e --no-serial --launch-first $lf > $O/bench_lf$lf.log 2>&1 || { tail -20 $O/bench_lf$lf.log; exit 1; }
+  python -c "import json;d=json.loads(open('$O/bench_lf$lf.log').read().strip().splitlines()[-1]);print('lf$lf', round(d['value']/1e6,2), round(d['ms_per_step'],4), d['breakdown']['host_issue_ms_per_step'])"
+done
