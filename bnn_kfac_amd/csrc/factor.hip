@@ -39,6 +39,7 @@ struct FactorJobDev {
   int accum;         // deferred reduction: `slab` is the caller's accumulator
   float sbeta;       // accumulator update: slab = sbeta*slab + alpha*partial
   char* split3;      // pre-split bf16x3 panel images of the job (kfac_factor_syrk3), else null
+  int x3pair;        // kfac_factor_tiles_x3: thin last tile row, diagonal + edge tiles paired
 };
 
 struct FactorArgs {
@@ -743,6 +744,21 @@ __global__ __launch_bounds__(NTHREADS, S3D_WGS) void kfac_factor_syrk3(FactorArg
 // tile into the syrk3 LDS image (x3m) lost (224 us).  The kernel is issue-bound: two
 // waves per SIMD keep its issue port ~90 % busy with 7.3 split VALU per MFMA.
 constexpr int X3_THREADS = 128;
+
+// kfac_factor_tiles_x3's work units of a factor of n over T = ceil(n / 64) tiles per
+// edge: the lower-triangle tiles, or with a thin last tile row (T >= 2 and at most 32
+// rows in it) the T-1 pairs (i, i) + (T-1, i), the other strictly lower tiles of rows
+// < T-1 and the corner (see X3_PAIR)
+static bool x3_pairing() {  // KFAC_X3_PAIR=0: no pairs (A/B)
+  static const bool on = [] {
+    const char* v = getenv("KFAC_X3_PAIR");
+    return v ? atoi(v) != 0 : true;
+  }();
+  return on;
+}
+static inline bool x3_thin(int n, int T) { return x3_pairing() && T >= 2 && n - TILE * (T - 1) <= 32; }
+__host__ __device__ inline int x3_units_of(int T, bool pair) { return T * (T + 1) / 2 - (pair ? T - 1 : 0); }
+static inline int x3_units(int n, int T) { return x3_units_of(T, x3_thin(n, T)); }
 constexpr int X3_NW = X3_THREADS / 64;
 
 struct X3Frag {
@@ -837,16 +853,27 @@ __device__ __forceinline__ void x3_pattern() {  // 6 MFMAs, NV VALU each, the re
   }
 }
 
+// X3_PAIR: a factor whose last tile row is thin (n - 64 (T-1) <= 32: one block row,
+// the MNIST MLP's 785 and 129) pairs diagonal tile (i, i) with edge tile (T-1, i) in ONE
+// task: fragments A0, A1 (panel i) and C0 (panel T-1, block 0), five blocks
+//   D00 = A0 A0, D10 = A1 A0, D11 = A1 A1 (tile (i, i)), E00 = C0 A0, E01 = C0 A1
+// -- 30 MFMAs on 3 fragments per 16 rows, where the diagonal task alone did 18 on 2
+// and the edge task 12 on 3 (both ran ahead of the full tiles, widening each XCD's
+// L2 working set), and T-1 fewer tasks per K-split.  acc[0][0] D00, acc[1][0] D10,
+// acc[1][1] D11, acc[0][1] E00, acc4 E01; called with ti = i, tj = T-1.
+constexpr int X3_PAIR = 16;
+
 template <int MASK, bool FILL>
 __device__ __forceinline__ void x3_loop(const FactorJobDev& J, const float* const* segs, int ti, int tj,
-                                        int64_t s0, int64_t s1, floatx16 (&acc)[2][2]) {
+                                        int64_t s0, int64_t s1, floatx16 (&acc)[2][2], floatx16& acc4) {
+  constexpr bool PAIR = MASK == X3_PAIR;
   constexpr bool A00 = MASK & 1, A01 = MASK & 2, A10 = MASK & 4, A11 = MASK & 8;
-  constexpr bool ROW1 = A10 || A11, COL1 = A01 || A11;
+  constexpr bool ROW1 = A10 || A11 || PAIR, COL1 = A01 || A11;
   // masks 13 and 1 occur on diagonal tiles only (an off-diagonal tile with block
   // (1, 1), or with any block, has (0, 1)): B fragments = A fragments
   constexpr bool SAME = MASK == 13 || MASK == 1;
-  static_assert(A00, "block (0, 0) always has work");
-  // fragments: 0 A block 0, 1 A block 1, 2 B block 0, 3 B block 1
+  static_assert(A00 || PAIR, "block (0, 0) always has work");
+  // fragments: 0 A block 0, 1 A block 1, 2 B block 0, 3 B block 1 (PAIR: 2 = C0)
   constexpr bool USE[4] = {true, ROW1, !SAME, !SAME && COL1};
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -943,7 +970,25 @@ __device__ __forceinline__ void x3_loop(const FactorJobDev& J, const float* cons
     c1 = c2;
     advance(c2);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (MASK == 15) {
+    if constexpr (PAIR) {  // B0 = C0
+      const X3Frag A1 = take(1, kc, c1);
+      x3_six(acc[0][0], A0, A0);
+      x3_pattern<NV>();
+      __builtin_amdgcn_sched_barrier(0);
+      A0n = take(0, kn, c2);
+      x3_six(acc[0][1], B0, A0);
+      x3_pattern<NV>();
+      __builtin_amdgcn_sched_barrier(0);
+      B0n = take(2, kn, c2);
+      x3_six(acc[1][0], A1, A0);
+      x3_pattern<NV>();
+      __builtin_amdgcn_sched_barrier(0);
+      x3_six(acc[1][1], A1, A1);
+      x3_pattern<0>();
+      __builtin_amdgcn_sched_barrier(0);
+      x3_six(acc4, B0, A1);
+      x3_pattern<0>();
+    } else if constexpr (MASK == 15) {
       const X3Frag A1 = take(1, kc, c1);
       x3_six(acc[0][0], A0, B0);
       x3_pattern<NV>();
@@ -1022,11 +1067,26 @@ template <int GBK, int NSLOT>
 __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const float* const* segs, int local,
                                                float* lds, int split_major) {
   static_assert(GBK == 16 * X3_NW, "one 16-row half stage per wave");
-  const int ntiles = J.t * (J.t + 1) / 2;
-  const int split = split_major ? local / ntiles : local % J.splits;
-  const int tile = split_major ? local - split * ntiles : local / J.splits;
+  const int T = J.t;
+  const bool thin = J.x3pair != 0;
+  const int units = x3_units_of(T, thin);
+  const int split = split_major ? local / units : local % J.splits;
+  const int unit = split_major ? local - split * units : local / J.splits;
   int ti, tj;
-  tri_decode(tile, ti, tj);
+  bool pair = false;
+  if (!thin) {
+    tri_decode(unit, ti, tj);
+  } else if (unit < T - 1) {  // pairs first: diagonal (i, i) with edge (T-1, i)
+    pair = true;
+    ti = unit;
+    tj = T - 1;
+  } else if (unit < T - 1 + (T - 1) * (T - 2) / 2) {  // strictly lower tiles of rows < T-1
+    tri_decode(unit - (T - 1), ti, tj);
+    ++ti;  // (row i of the strict lower triangle has i tiles: tri index of (i-1, j))
+  } else {  // the corner (T-1, T-1)
+    ti = tj = T - 1;
+  }
+  const int tile = ti * (ti + 1) / 2 + (pair ? ti : tj);  // (a pair's: its diagonal tile)
   const int64_t s0 = (int64_t)split * J.chunk;
   const int64_t s1 = min(J.nst, s0 + J.chunk);
   const int lane = threadIdx.x & 63;
@@ -1044,13 +1104,16 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
 #if KFAC_X3_AB_FULL  // timing A/B only: every tile runs the full-tile loop (balance probe)
   mask = 15;
 #endif
-  floatx16 acc[2][2];
+  if (pair) mask = X3_PAIR;
+  floatx16 acc[2][2], acc4;
 #pragma unroll
   for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
     for (int bj = 0; bj < 2; ++bj)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[bi][bj][v] = 0.f;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc4[v] = 0.f;
   X3_STAMP(1, wall_clock64());
   X3_STAMP(4, __builtin_amdgcn_s_memtime());
   X3_STAMP(7, (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) | (mask << 8) | ((uint32_t)(s1 - s0) << 16));
@@ -1060,10 +1123,11 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
     const bool fill = J.x.ones >= 0 && ((J.x.ones >> 6) == ti || (J.x.ones >> 6) == tj);
 #define X3_CASE(M)                                                   \
   case M:                                                            \
-    if (fill) x3_loop<M, true>(J, segs, ti, tj, s0, s1, acc);        \
-    else x3_loop<M, false>(J, segs, ti, tj, s0, s1, acc);            \
+    if (fill) x3_loop<M, true>(J, segs, ti, tj, s0, s1, acc, acc4);  \
+    else x3_loop<M, false>(J, segs, ti, tj, s0, s1, acc, acc4);      \
     break;
     switch (mask) {  // (block (0, 0) always has work)
+      X3_CASE(X3_PAIR)
       X3_CASE(15)
       X3_CASE(13)  // diagonal
       X3_CASE(5)
@@ -1075,6 +1139,48 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
   }
   X3_STAMP(2, wall_clock64());
   X3_STAMP(5, __builtin_amdgcn_s_memtime());
+  if (pair) {
+    // wave 0 keeps D00, E00, E01 and wave 1 D10, D11; each hands the other's through
+    // LDS slots [D00, D10, D11, E00, E01][16 values][64 lanes]; sums are w0 + w1
+    __syncthreads();
+    float* xo = lds;
+    auto put = [&](int sl, const floatx16& a) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) xo[(sl * 16 + v) * 64 + lane] = a[v];
+    };
+    auto add = [&](int sl, floatx16& a) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) a[v] += xo[(sl * 16 + v) * 64 + lane];
+    };
+    float* outD = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE;
+    float* outE = J.slab + ((size_t)((T - 1) * T / 2 + ti) * J.splits + split) * TILE * TILE;
+    auto store = [&](float* o, int bi, int bj, const floatx16& a) {
+      put_partial(J, a, [&](int v) { return &o[(bi * 32 + acc_row(v, lane)) * TILE + bj * 32 + (lane & 31)]; });
+    };
+    if (wave == 0) {
+      put(1, acc[1][0]);
+      put(2, acc[1][1]);
+    } else {
+      put(0, acc[0][0]);
+      put(3, acc[0][1]);
+      put(4, acc4);
+    }
+    __syncthreads();
+    if (wave == 0) {
+      add(0, acc[0][0]);
+      add(3, acc[0][1]);
+      add(4, acc4);
+      store(outD, 0, 0, acc[0][0]);
+      store(outE, 0, 0, acc[0][1]);
+      store(outE, 0, 1, acc4);
+    } else {
+      add(1, acc[1][0]);
+      add(2, acc[1][1]);
+      store(outD, 1, 0, acc[1][0]);
+      store(outD, 1, 1, acc[1][1]);
+    }
+    return;
+  }
   // wave w stores block row w: it hands the other block row's partials to the other
   // wave through LDS (the ring is free after the barrier), then adds the other
   // wave's.  Both sums are w0 + w1 (IEEE addition commutes): deterministic.
@@ -1111,8 +1217,8 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
 // 2 waves per SIMD (178 VGPRs): 4 workgroups per CU leave a 32-tile inversion
 // workgroup (107 registers, 29 KB) room to run beside the pass
 __global__ __launch_bounds__(X3_THREADS, 2) void kfac_factor_tiles_x3(FactorArgs args) {
-  // (LDS only for the epilogue's hand-off of a block row, 16 KB)
-  __shared__ __attribute__((aligned(16))) float lds[2 * BK * TILE];
+  // (LDS only for the epilogue's hand-off: a block row, 16 KB; a pair's blocks, 20 KB)
+  __shared__ __attribute__((aligned(16))) float lds[5 * 16 * 64];
   X3_STAMP(0, wall_clock64());
   X3_STAMP(6, (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4));
   for (int i = 0; i < args.stagger * (int)(blockIdx.x >> 8); ++i) __builtin_amdgcn_s_sleep(8);
@@ -1922,11 +2028,13 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
   int64_t max_steps = 1;
   for (int i = 0; i < njobs; ++i) max_steps = std::max(max_steps, job_stages(jobs[i]));
   int64_t units[MAXJ];
+  const bool x3 = !s3 && tiles_x3_group(jobs, njobs);
   for (int i = 0; i < njobs; ++i) {
     const int64_t t = cdiv(factor_n(jobs[i]), TILE);
     const int64_t t3 = cdiv(factor_n(jobs[i]), MT);
     ConvGeom cg;
     if (s3) units[i] = factor_n(jobs[i]) <= 32 ? 1 : t3 * (t3 + 1) / 2;
+    else if (x3) units[i] = x3_units((int)factor_n(jobs[i]), (int)t);
     else units[i] = conv_geom(jobs[i], cg) ? cg.units : t * (t + 1) / 2;
   }
   // workgroups of job i at `splits` K-splits
@@ -1941,8 +2049,11 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
     const char* v = getenv("KFAC_SYRK_ROUNDS");
     return v ? atoi(v) : 0;
   }();
+  // (kfac_factor_tiles_x3: one round -- MNIST MLP with thin-row pairs, same box: 163.4
+  // vs 170.3 / 167.4 us per launch at the two rounds the cost model picks)
+  const int64_t max_rounds = x3 ? 1 : 4;
   for (int64_t r = 1; r <= 8; ++r) {
-    if (forced_rounds > 0 ? r != forced_rounds : r > 4) continue;
+    if (forced_rounds > 0 ? r != forced_rounds : r > max_rounds) continue;
     int64_t lo = MIN_CHUNK, hi = std::max(MIN_CHUNK, max_steps);
     if (tasks_at(hi) > r * slots) continue;  // even one split per tile needs more rounds
     while (lo < hi) {
@@ -2072,6 +2183,7 @@ static int prepare_group(const kfac_factor_job* jobs, int njobs, char* ws, size_
     FactorJobDev& d = args.job[i];
     fill_dev(d, jb);
     d.glds = job_glds(jb);
+    d.x3pair = tiles_x3_group(jobs, njobs) && x3_thin(d.n, d.t);
     d.splits = plans[i].splits;
     d.chunk = plans[i].chunk;
     if (d.nseg > 1) {  // kfac_factor_update keeps a launch within KSEG batch bases
