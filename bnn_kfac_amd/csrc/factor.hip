@@ -2171,7 +2171,13 @@ static int prepare_group(const kfac_factor_job* jobs, int njobs, char* ws, size_
   args = FactorArgs{};
   red = FactorArgs{};
   args.njobs = njobs;
-  args.stagger = 5;
+  {
+    static const int stagger = [] {  // (A/B: KFAC_SYRK_STAGGER)
+      const char* e = getenv("KFAC_SYRK_STAGGER");
+      return e ? atoi(e) : 5;
+    }();
+    args.stagger = stagger;
+  }
   {
     const char* e = getenv("KFAC_SYRK_ORDER");
     args.split_major = e ? atoi(e) : 1;
