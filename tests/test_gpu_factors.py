@@ -277,6 +277,58 @@ def test_multibatch_job_raw_abi(hip_device, cols, rows, offset, ones, deferred):
     np.testing.assert_array_equal(F.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("deferred", [False, True])
+def test_x3_thin_row_pairs_exact(hip_device, deferred):
+    """kfac_factor_tiles_x3's work units (one launch: the group's largest factor, 785,
+    selects it; every operand 16-byte rows): factors whose last tile row is thin (785:
+    17 rows, 129: 1, 93: 29, 65: 1) run their diagonal tiles paired with the edge tiles
+    below them, 97 (33 rows), 128 and 33 (one tile) do not; multi-batch operands with a
+    ragged last stage; exact on small integers against the fp64 sum."""
+    from bnn_kfac_amd import _native as N
+    rng = np.random.default_rng(7)
+    nseg, rows = 3, 1000
+    cases = [(784, True), (128, True), (92, True), (64, True), (96, True), (32, True), (128, False)]
+    jobs, want, keep, outs, accs = [], [], [], [], []
+    for cols, ones in cases:
+        xs = [rng.integers(-3, 4, size=(rows, cols)).astype(np.float32) for _ in range(nseg)]
+        views = [_t(x, hip_device) for x in xs]
+        keep.append(views)
+        n = cols + ones
+        F = torch.full((n, n), np.nan, device=hip_device)
+        outs.append(F)
+        table = N.segment_table([v.data_ptr() for v in views])
+        keep.append(table)
+        job = N.factor_job(N.rowmajor_operand(views[0], ones), F, 1.0, 0.0)
+        job.seg_ptrs, job.nseg = N.table_ptr(table), nseg
+        jobs.append(job)
+        w = np.zeros((n, n))
+        for x in xs:
+            xo = np.concatenate([x, np.ones((rows, 1), np.float32)], 1) if ones else x
+            w += xo.T.astype(np.float64) @ xo
+        want.append(w)
+    N.profile_reset()
+    N.profile_enable(True)
+    if deferred:
+        plan = N.factor_accum_plan(jobs)
+        flush = []
+        for job, (splits, nbytes) in zip(jobs, plan):
+            acc = torch.empty(nbytes, dtype=torch.uint8, device=hip_device)
+            accs.append(acc)
+            job.acc, job.acc_splits, job.acc_beta = acc.data_ptr(), splits, 0.0
+            f = N.FactorJob.from_buffer_copy(job)
+            f.seg_ptrs, f.nseg = None, 0
+            flush.append(f)
+        N.factor_update(jobs, hip_device)
+        N.factor_flush(flush, hip_device)
+    else:
+        N.factor_update(jobs, hip_device)
+    torch.cuda.synchronize()
+    N.profile_enable(False)
+    assert N.profile_read(N.PROF_FACTOR_X3)[1] == 1  # one kfac_factor_tiles_x3 launch
+    for F, w in zip(outs, want):
+        np.testing.assert_array_equal(F.cpu().numpy(), w)
+
+
 def test_queued_pass_matches_per_batch_launches(hip_device):
     """KFAC's default queued pass (multi-batch jobs, one short last batch, separate
     record allocations) equals launching every update on its own."""
