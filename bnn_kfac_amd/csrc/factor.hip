@@ -849,7 +849,8 @@ __device__ __forceinline__ void x3_pattern() {  // 6 MFMAs, NV VALU each, the re
   for (int i = 0; i < 6; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);       // MFMA
     if (NV > 0) __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);  // VALU
-    if (i < 4) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);    // VMEM read
+    // (all 8 reloads after the first MFMA: 170 vs 159-166 us, profiles/r04v/)
+    if (i < 4) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);  // VMEM read
   }
 }
 
@@ -962,6 +963,7 @@ __device__ __forceinline__ void x3_loop(const FactorJobDev& J, const float* cons
   // each stage (with the prologue's loads still in flight it merged them into a
   // vmcnt(0) there, exposing a whole stage of load latency)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // (6 / 11 VALU slots per MFMA measured equal within the box's +-4 us, profiles/r04v/)
   constexpr int NV = FILL ? 52 / 6 + 1 : 44 / 6 + 1;
   // one stage: P = (A0, B0) of this stage in, (A0', B0') of the next stage out
   auto stage = [&](const X3Frag& A0, const X3Frag& B0, X3Frag& A0n, X3Frag& B0n) {
