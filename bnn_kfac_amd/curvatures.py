@@ -18,6 +18,7 @@ views into it), so a data-parallel pass needs exactly one all-reduce
 from __future__ import annotations
 
 import copy
+import os
 from abc import ABC, abstractmethod
 from typing import Any, List, NamedTuple, Union
 
@@ -145,6 +146,10 @@ class Curvature(ABC):
         self.inv_state = {modules[k]: tuple(v) if isinstance(v, list) else v
                           for k, v in blob['inv_state'].items()}
         print('Loading %s complete!\n' % filename)
+
+
+# A/B: KFAC_SKIP_DONE_WAITS=0 keeps a stream wait on events the host has seen complete
+_SKIP_DONE_WAITS = os.environ.get("KFAC_SKIP_DONE_WAITS", "1") != "0"
 
 
 def _same_shapes(f, g):
@@ -277,7 +282,9 @@ class KFAC(Curvature):
             return
         ev = self._buf_read.pop(buf.data_ptr(), None)
         if ev is not None:
-            self._wait(ev, stream, buf.device)
+            # (an event the host already sees complete needs no wait packet on the stream)
+            if not (_SKIP_DONE_WAITS and isinstance(ev, N.RawEvent) and ev.query()):
+                self._wait(ev, stream, buf.device)
             self._pool_event(buf.device, ev)  # the wait captured its record: reusable
 
     def flush(self):
@@ -799,15 +806,17 @@ class KFAC(Curvature):
         return s[self._inv_turn]
 
     @classmethod
-    def _order_after(cls, pending):
+    def _order_after(cls, pending, settled=False):
         """Later work on the caller's stream sees the inversion's factors (no host wait).
         KFAC.invert allocates the factors on the caller's stream, so their release is
         ordered after this wait too; factors allocated on another stream (the sharded
-        inversion's torch events) are also recorded on the caller's stream."""
+        inversion's torch events) are also recorded on the caller's stream.  `settled`:
+        the host has already waited for `done` (a raw event then needs no wait packet)."""
         if pending.on_side:
             dev = pending.outs[0].device
             if isinstance(pending.done, N.RawEvent):
-                pending.done.wait_on(N.stream_handle(dev))
+                if not (settled and _SKIP_DONE_WAITS):
+                    pending.done.wait_on(N.stream_handle(dev))
             else:
                 cur = torch.cuda.current_stream(dev)
                 cur.wait_event(pending.done)
@@ -825,8 +834,10 @@ class KFAC(Curvature):
             self._inv_older.append(pending)
         while self._inv_older and (len(self._inv_older) > self.max_pending or self._inv_older[0].done.query()):
             p = self._inv_older.pop(0)
-            self._order_after(p)
+            # the verdict's host wait first (it settles `done`, also when it raises:
+            # the factors are complete either way), then the stream order
             self._verdict(p)
+            self._order_after(p, settled=True)
 
     def _check_inverse(self):
         """Settle every pending inversion, oldest first: a factor that is not positive
