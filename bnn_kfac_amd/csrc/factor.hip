@@ -832,9 +832,6 @@ __device__ __forceinline__ X3Frag x3_split8(const float (&x)[8]) {
 // the buffer's record limit (0), and the ones column (FILL: only the tasks whose
 // fragments hold it) is a select of 1 / 0 by row validity.
 // Microbench: tools/microbench/x3w_mb.hip; DESIGN.md §3.1c.
-#ifndef KFAC_X3_AB_FULL
-#define KFAC_X3_AB_FULL 0
-#endif
 #ifndef KFAC_X3_AB
 #define KFAC_X3_AB 0  // timing A/B builds (tools/build_ab.sh): 1 no reloads, 2 no split, 3 neither
 #endif
@@ -1103,9 +1100,6 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
       act[bi][bj] = !(same && bi < bj) && ti * TILE + bi * 32 < J.n && tj * TILE + bj * 32 < J.n;
       mask |= act[bi][bj] << (2 * bi + bj);
     }
-#if KFAC_X3_AB_FULL  // timing A/B only: every tile runs the full-tile loop (balance probe)
-  mask = 15;
-#endif
   if (pair) mask = X3_PAIR;
   floatx16 acc[2][2], acc4;
 #pragma unroll
