@@ -399,6 +399,9 @@ class KFAC(Curvature):
             off += nG * nG
             views[layer] = (A, G)
         self._packed, self._packed_views = buf, views
+        # fast-path templates onto a dropped buffer's views can never match again
+        alt = self._alt_packed.data_ptr() if self._alt_packed is not None else None
+        self._fast_cache = {k: v for k, v in self._fast_cache.items() if k == alt}
 
     def _target(self, layer, nA, nG, device):
         """(A, G, beta): where this update writes and whether it accumulates."""
