@@ -503,7 +503,8 @@ __device__ __forceinline__ uint32_t bf16_pair(float a, float b) {
 }
 
 // x - y as one v_sub_f32 (the compiler would pair the subtractions into
-// v_pk_add_f32, which costs ~6x its issue slot beside MFMAs on gfx950)
+// v_pk_add_f32, which costs ~6x its issue slot beside MFMAs on gfx950; round 4, the
+// residual pairs as explicit v_pk_add_f32: 169-171 vs 165-167 us per MLP launch)
 __device__ __forceinline__ float sub_f32(float x, float y) {
   float r;
   asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
