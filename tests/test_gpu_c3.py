@@ -83,3 +83,45 @@ def test_lenet5_c3_pass_and_invert_vs_fp64_oracle(hip_device):
             np.testing.assert_allclose(L, ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max(),
                                        err_msg=f"layer {li} {name}")
             assert np.all(np.triu(L, 1) == 0)
+
+
+@pytest.mark.parametrize("config", ["lenet", "mlp"])
+def test_repeated_passes_fast_path_bit_identical(hip_device, config):
+    """The bench's loop (reset, a pass of updates with a short last batch, invert) four
+    times over the same records: from the third pass on no update takes the slow path
+    (cached per-buffer templates start each cycle, the short batch has its own), the
+    double-buffered state alternates, and every pass's factors and L factors are
+    bit-identical to the first pass's (deterministic kernels, same inputs)."""
+    from bnn_kfac_amd.curvatures import KFAC
+    images, batch = (8 * 1024 + 300, 1024) if config == "lenet" else (6 * 4096 + 1000, 4096)
+    specs = bench.CONFIGS[config]
+    net = bench.build_model(config, hip_device)
+    layers = [m for m in net.modules() if isinstance(m, (torch.nn.Linear, torch.nn.Conv2d))]
+    recs = bench.synthetic_records(specs, images, hip_device, seed=5)
+    kfac = KFAC(net)
+    kfac.launch_first = 16
+    slow = []
+    orig = KFAC._remember
+
+    def counting(self, *a, **k):
+        slow.append(1)
+        return orig(self, *a, **k)
+    KFAC._remember = counting
+    try:
+        per_pass, results = [], []
+        for _ in range(4):
+            n0 = len(slow)
+            kfac.reset()
+            for i in range(0, images, batch):
+                for layer, (a, g) in zip(layers, recs):
+                    kfac.record[layer] = [a[i:i + batch], g[i:i + batch]]
+                kfac.update(batch_size=min(batch, images - i))
+            kfac.invert(0.2 ** 2, 200)
+            per_pass.append(len(slow) - n0)
+            results.append([t.clone() for m in layers for t in list(kfac.state[m]) + list(kfac.inv_state[m])])
+    finally:
+        KFAC._remember = orig
+    assert per_pass[2:] == [0, 0], per_pass
+    for later in results[1:]:
+        for a, b in zip(results[0], later):
+            assert torch.equal(a, b)
