@@ -1,7 +1,7 @@
 # Round 4: the committed tree -- GPU suite, smoke, default bench lines (MLP x2, LeNet, wide)
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r04t
+O=gpurun_out/${TAG:-r04t}
 mkdir -p $O
 summ() { python -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);r=d['roofline'];print(sys.argv[2], round(d['value']/1e6,3),'M img/s', round(d['ms_per_step'],4),'ms', round(r['avg_launch_us'],1),'us', round(r['frac'],3), d['breakdown'].get('host_issue_ms_per_step'), d.get('serial_images_per_s'))" "$@"; }
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
