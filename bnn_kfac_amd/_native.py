@@ -39,7 +39,7 @@ class Operand(ctypes.Structure):
 class FactorJob(ctypes.Structure):
     _fields_ = [("x", Operand), ("alpha", c_f32), ("beta", c_f32), ("F", c_vp), ("ldF", c_i64),
                 ("acc", c_vp), ("acc_splits", c_i32), ("acc_beta", c_f32),
-                ("seg_ptrs", c_vp), ("nseg", c_i32), ("reserved2", c_i32)]
+                ("seg_ptrs", c_vp), ("nseg", c_i32), ("acc_stride", c_i32)]
 
 
 class InvertJob(ctypes.Structure):

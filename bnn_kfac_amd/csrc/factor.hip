@@ -40,6 +40,7 @@ struct FactorJobDev {
   float sbeta;       // accumulator update: slab = sbeta*slab + alpha*partial
   char* split3;      // pre-split bf16x3 panel images of the job (kfac_factor_syrk3), else null
   int x3pair;        // kfac_factor_tiles_x3: thin last tile row, diagonal + edge tiles paired
+  int sstride;       // slabs per tile of `slab` (a job's split s of tile t: t * sstride + s)
 };
 
 struct FactorArgs {
@@ -54,6 +55,7 @@ struct FactorArgs {
   // XCD whole K-ranges of all factors (KFAC_X3_INTERLEAVE)
   int interleave;
   int unit_end[MAXJ];
+  int main_tasks;  // kfac_factor_tiles_x3: tasks before the tail jobs' (XCD-mapped), the rest in dispatch order
   FactorJobDev job[MAXJ];
 };
 
@@ -160,11 +162,11 @@ __device__ __forceinline__ void factor_task(const FactorJobDev& J, const float* 
                                   diag, active, lds, acc, narrow);
   }
   if (narrow) {
-    store_narrow(J, J.slab + ((size_t)tile * J.splits + split) * TILE * TILE, acc, lds);
+    store_narrow(J, J.slab + ((size_t)tile * J.sstride + split) * TILE * TILE, acc, lds);
     return;
   }
   if (!active) return;
-  float* out = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE + qi * 32 * TILE + qj * 32;
+  float* out = J.slab + ((size_t)tile * J.sstride + split) * TILE * TILE + qi * 32 * TILE + qj * 32;
   put_partial(J, acc, [&](int v) { return &out[acc_row(v, lane) * TILE + (lane & 31)]; });
 }
 
@@ -409,11 +411,11 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, const fl
   }
   if (narrow) {  // (narrow => one tile, diagonal: A and B panels are the same)
     __syncthreads();
-    store_narrow(J, J.slab + ((size_t)tile * J.splits + split) * TILE * TILE, acc, lds);
+    store_narrow(J, J.slab + ((size_t)tile * J.sstride + split) * TILE * TILE, acc, lds);
     return;
   }
   if (!active) return;
-  float* out = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE + qi * 32 * TILE + qj * 32;
+  float* out = J.slab + ((size_t)tile * J.sstride + split) * TILE * TILE + qi * 32 * TILE + qj * 32;
   put_partial(J, acc, [&](int v) { return &out[acc_row(v, lane) * TILE + (lane & 31)]; });
 }
 
@@ -705,7 +707,7 @@ __device__ __forceinline__ void s3d_task(const FactorJobDev& J, int local, char*
     }
   }
   const int ti = 2 * I + wr, tj = 2 * Jc + wc;
-  float* o = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.splits + split) * TILE * TILE;
+  float* o = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.sstride + split) * TILE * TILE;
 #pragma unroll
   for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
@@ -750,6 +752,13 @@ constexpr int X3_THREADS = 128;
 // edge: the lower-triangle tiles, or with a thin last tile row (T >= 2 and at most 32
 // rows in it) the T-1 pairs (i, i) + (T-1, i), the other strictly lower tiles of rows
 // < T-1 and the corner (see X3_PAIR)
+static bool x3_merge() {  // KFAC_X3_TAIL=0: tail jobs ordered and planned like the others (A/B)
+  static const bool on = [] {
+    const char* v = getenv("KFAC_X3_TAIL");
+    return v ? atoi(v) != 0 : true;
+  }();
+  return on;
+}
 static bool x3_pairing() {  // KFAC_X3_PAIR=0: no pairs (A/B)
   static const bool on = [] {
     const char* v = getenv("KFAC_X3_PAIR");
@@ -1149,8 +1158,8 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
 #pragma unroll
       for (int v = 0; v < 16; ++v) a[v] += xo[(sl * 16 + v) * 64 + lane];
     };
-    float* outD = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE;
-    float* outE = J.slab + ((size_t)((T - 1) * T / 2 + ti) * J.splits + split) * TILE * TILE;
+    float* outD = J.slab + ((size_t)tile * J.sstride + split) * TILE * TILE;
+    float* outE = J.slab + ((size_t)((T - 1) * T / 2 + ti) * J.sstride + split) * TILE * TILE;
     auto store = [&](float* o, int bi, int bj, const floatx16& a) {
       put_partial(J, a, [&](int v) { return &o[(bi * 32 + acc_row(v, lane)) * TILE + bj * 32 + (lane & 31)]; });
     };
@@ -1183,7 +1192,7 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
   // wave's.  Both sums are w0 + w1 (IEEE addition commutes): deterministic.
   __syncthreads();
   float* xo = lds;  // [wave][bj][16 values][64 lanes]
-  float* out = J.slab + ((size_t)tile * J.splits + split) * TILE * TILE;
+  float* out = J.slab + ((size_t)tile * J.sstride + split) * TILE * TILE;
   auto hand = [&](auto bic) {
     constexpr int bi = decltype(bic)::value;
 #pragma unroll
@@ -1218,8 +1227,11 @@ __global__ __launch_bounds__(X3_THREADS, 2) void kfac_factor_tiles_x3(FactorArgs
   __shared__ __attribute__((aligned(16))) float lds[5 * 16 * 64];
   X3_STAMP(0, wall_clock64());
   X3_STAMP(6, (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4));
+  X3_STAMP(7, 0);  // (narrow tasks leave it 0; x3 tasks overwrite it)
   for (int i = 0; i < args.stagger * (int)(blockIdx.x >> 8); ++i) __builtin_amdgcn_s_sleep(8);
-  const int task = xcd_task(blockIdx.x, gridDim.x);
+  // the main jobs' tasks XCD-contiguous (xcd_task), the tail jobs' in dispatch order:
+  // they start as the main tasks end, on every XCD
+  const int task = (int)blockIdx.x < args.main_tasks ? xcd_task(blockIdx.x, args.main_tasks) : (int)blockIdx.x;
   int j = 0, local;
   if (args.interleave) {  // task = split * U + unit of the concatenated jobs' units
     const int U = args.unit_end[args.njobs - 1];
@@ -1609,7 +1621,7 @@ __global__ __launch_bounds__(NTHREADS, (CB == 2 && !M3) ? KFAC_CONV_OCC : 4) voi
   for (int i = 0; i < CB; ++i) {
     if (i >= nmine) break;
     const int bi = bij[i] >> 16, bj = bij[i] & 0xffff, ti = bi >> 1, tj = bj >> 1;
-    float* o = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.splits + split) * TILE * TILE +
+    float* o = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.sstride + split) * TILE * TILE +
                (bi & 1) * 32 * TILE + (bj & 1) * 32;
     put_partial(J, acc[i], [&](int v) { return &o[acc_row(v, lane) * TILE + (lane & 31)]; });
   }
@@ -1860,7 +1872,7 @@ __global__ __launch_bounds__(NTHREADS) void kfac_factor_reduce(FactorArgs args) 
   const int part = threadIdx.x >> 6, f = threadIdx.x & 63;  // f: float4 of the 4 x 64 strip
   const int r = f >> 4, c4 = (f & 15) * 4;
   const float4* slab =
-      reinterpret_cast<const float4*>(J.slab + (size_t)tile * J.splits * TILE * TILE) +
+      reinterpret_cast<const float4*>(J.slab + (size_t)tile * J.sstride * TILE * TILE) +
       (((s0 + r) * TILE + c4) >> 2);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   const int S = J.splits;
@@ -2011,6 +2023,16 @@ static bool tiles_x3_group(const kfac_factor_job* jobs, int njobs) {
   return nmax >= (tiles_x3_mode() == 1 ? 33 : 512);
 }
 
+// A tail job of a kfac_factor_tiles_x3 group: fewer than half the stages of the
+// group's largest job (a pass's short last batch beside its multi-batch full batches).
+// Its tasks are dispatched after the others' and are not counted against the slots.
+static bool x3_tail(const kfac_factor_job* jobs, int njobs, int i, bool x3) {
+  if (!x3 || !x3_merge()) return false;
+  int64_t mx = 0;
+  for (int k = 0; k < njobs; ++k) mx = std::max(mx, job_stages(jobs[k]));
+  return 2 * job_stages(jobs[i]) < mx;
+}
+
 static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
                       int64_t slots = 0) {
   const bool s3 = syrk3_group(jobs, njobs);
@@ -2036,9 +2058,23 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
   }
   // workgroups of job i at `splits` K-splits
   auto job_tasks = [&](int i, int64_t splits) { return units[i] * splits; };
+  // kfac_factor_tiles_x3: a narrow job (n <= 32, one fp32-MFMA tile, latency-bound
+  // direct loads) takes X3_NARROW_SPLIT times the K-splits of the chunk, so its few
+  // tasks end well before the bf16x3 tiles' (MNIST MLP G2: ~230 us of a 270 us launch
+  // at the common chunk)
+  static const int64_t narrow_f = [] {
+    const char* v = getenv("KFAC_X3_NARROW");
+    return (int64_t)(v ? std::max(1, atoi(v)) : 4);
+  }();
+  auto job_splits = [&](int i, int64_t c) {
+    const int64_t st = job_stages(jobs[i]);
+    const int64_t sp = cdiv(st, c);
+    return x3 && factor_n(jobs[i]) <= 32 ? std::min(st, sp * narrow_f) : sp;
+  };
   auto tasks_at = [&](int64_t c) {
     int64_t n = 0;
-    for (int i = 0; i < njobs; ++i) n += job_tasks(i, cdiv(job_stages(jobs[i]), c));
+    for (int i = 0; i < njobs; ++i)
+      if (!x3_tail(jobs, njobs, i, x3)) n += job_tasks(i, job_splits(i, c));
     return n;
   };
   int64_t best_c = std::max(MIN_CHUNK, max_steps), best_cost = -1;
@@ -2073,7 +2109,7 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
       p.tasks = (int)job_tasks(i, p.splits);
       continue;
     }
-    p.splits = (int)cdiv(steps, best_c);
+    p.splits = (int)job_splits(i, best_c);
     static const int forced_splits = [] {  // (tuning experiments: KFAC_SYRK_SPLITS)
       const char* v = getenv("KFAC_SYRK_SPLITS");
       return v ? atoi(v) : 0;
@@ -2159,8 +2195,20 @@ struct GroupLaunch {
   int tasks, rtiles, split_tasks;
 };
 
-static int prepare_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t ws_bytes,
+static int prepare_group(const kfac_factor_job* jobs_in, int njobs, char* ws, size_t ws_bytes,
                          GroupLaunch& g) {
+  // kfac_factor_tiles_x3: the tail jobs (x3_tail) go last, their workgroups dispatched
+  // after the others' (see kfac_factor_tiles_x3) -- a pass's short last batch fills the
+  // slots its full batches' tasks free at the end of the launch
+  const bool x3 = tiles_x3_group(jobs_in, njobs);
+  kfac_factor_job perm[MAXJ];
+  int nmain = 0;
+  for (int pass = 0; pass < 2; ++pass)
+    for (int i = 0; i < njobs; ++i)
+      if (x3_tail(jobs_in, njobs, i, x3) == (pass == 1)) perm[nmain++] = jobs_in[i];
+  nmain = 0;
+  for (int i = 0; i < njobs; ++i) nmain += !x3_tail(jobs_in, njobs, i, x3);
+  const kfac_factor_job* jobs = perm;
   Plan plans[MAXJ];
   plan_jobs(jobs, njobs, plans);
   FactorArgs& args = g.args;
@@ -2188,6 +2236,7 @@ static int prepare_group(const kfac_factor_job* jobs, int njobs, char* ws, size_
     d.glds = job_glds(jb);
     d.x3pair = tiles_x3_group(jobs, njobs) && x3_thin(d.n, d.t);
     d.splits = plans[i].splits;
+    d.sstride = jb.acc && jb.acc_stride > 0 ? jb.acc_stride : d.splits;
     d.chunk = plans[i].chunk;
     if (d.nseg > 1) {  // kfac_factor_update keeps a launch within KSEG batch bases
       const float* const* bases = reinterpret_cast<const float* const*>(jb.seg_ptrs);
@@ -2208,7 +2257,9 @@ static int prepare_group(const kfac_factor_job* jobs, int njobs, char* ws, size_
     d.task_begin = tasks;
     tasks += plans[i].tasks;
     args.task_end[i] = tasks;
+    if (i == nmain - 1) args.main_tasks = tasks;
   }
+  if (nmain == njobs || nmain == 0) args.main_tasks = tasks;
   g.tasks = tasks;
   g.rtiles = rtiles;
   g.split_tasks = 0;
@@ -2362,6 +2413,8 @@ static int validate(const kfac_factor_job* jobs, int njobs) {
     if (!valid_operand(j.x) || !j.F || j.ldF < factor_n(j)) return KFAC_EINVAL;
     if ((int64_t)factor_n(j) > (int64_t)1 << 20) return KFAC_EINVAL;
     if (j.acc && (j.acc_splits <= 0 || j.acc_splits > (1 << 20))) return KFAC_EINVAL;
+    if (j.acc && j.acc_stride != 0 && (j.acc_stride < j.acc_splits || j.acc_stride > (1 << 20)))
+      return KFAC_EINVAL;
     if (j.nseg < 0 || (j.nseg > 1 && !j.seg_ptrs) || job_sps(j) > (1 << 30))
       return KFAC_EINVAL;
   }
@@ -2474,6 +2527,7 @@ extern "C" int kfac_factor_flush(const kfac_factor_job* jobs, int njobs, kfac_st
     fill_dev(e, jb);
     e.slab = jb.acc;
     e.splits = jb.acc_splits;
+    e.sstride = jb.acc_stride > 0 ? jb.acc_stride : jb.acc_splits;
     e.tile_begin = tiles;
     tiles += e.t * (e.t + 1) / 2;
     red.tile_end[red.njobs++] = tiles;

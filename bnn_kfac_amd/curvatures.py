@@ -148,8 +148,13 @@ class Curvature(ABC):
         print('Loading %s complete!\n' % filename)
 
 
+# bytes of one 64 x 64 fp32 partial tile: a slab range starting at split s0 of an
+# accumulator starts s0 tiles into it (kfac_factor_job.acc_stride)
+_SLAB_BYTES = 64 * 64 * 4
+
 # A/B: KFAC_SKIP_DONE_WAITS=0 keeps a stream wait on events the host has seen complete
 _SKIP_DONE_WAITS = os.environ.get("KFAC_SKIP_DONE_WAITS", "1") != "0"
+_MERGE_LAUNCHES = os.environ.get("KFAC_MERGE_LAUNCHES", "1") != "0"
 
 
 def _same_shapes(f, g):
@@ -256,6 +261,8 @@ class KFAC(Curvature):
         # eager_verdict False: inversions whose verdict may stay unread (and whose
         # factors stay queued) before invert() waits for the oldest one
         self.max_pending = 2
+        # one launch for the groups of a queued flush (full batches + short last one)
+        self.merge_launches = _MERGE_LAUNCHES
         self._inv_streams = {}    # device index -> side streams
 
     def reset(self):
@@ -618,6 +625,7 @@ class KFAC(Curvature):
                 groups.append(queue[start:i])
                 start = i
         tables = []
+        launches = []
         for group in groups:
             tmpl = group[0][0]
             jobs = []
@@ -636,6 +644,15 @@ class KFAC(Curvature):
                         if i:
                             job.beta = 1.0  # later batches add to the first one's result
                         jobs.append(job)
+            launches.append(jobs)
+        # the groups of a flush (a pass's full batches and its short last one) as ONE
+        # launch, each factor's jobs on their own accumulator slab ranges, when the
+        # pending cycle's accumulators have a range for every job (or a new cycle
+        # starts here); else one launch per group
+        merged = [j for jobs in launches for j in jobs]
+        if len(launches) > 1 and self.merge_launches and self._acc_takes(merged, device):
+            launches = [merged]
+        for jobs in launches:
             self._defer(jobs, device)
             N.factor_update(jobs, device)
         # queued records are released here (the host segment tables were read by the
@@ -643,41 +660,63 @@ class KFAC(Curvature):
         # the launches on this stream
         del tables, queue
 
+    def _acc_takes(self, jobs, device):
+        """A launch of `jobs` fits the pending accumulation cycle: every factor it
+        writes has an accumulator there, with a slab range per job of that factor."""
+        if self._acc_map is None:
+            return True
+        if device != self._acc_device:
+            return False
+        count = {}
+        for j in jobs:
+            count[j.F] = count.get(j.F, 0) + 1
+        return all(F in self._acc_map and n <= len(self._acc_map[F][1]) for F, n in count.items())
+
     def _defer(self, jobs, device):
         """Point each job at its factor's accumulator: continue the pending cycle when
-        it already holds every target factor, else flush and plan a new cycle for this
-        launch's shapes (one accumulator per distinct factor)."""
-        if self._acc_map is not None and (device != self._acc_device or
-                                          any(j.F not in self._acc_map for j in jobs)):
+        it holds a slab range for every job, else flush and plan a new cycle for this
+        launch's jobs.  A factor written by k jobs of one launch gets k slab ranges of
+        one accumulator (kfac_factor_job.acc_stride: the ranges' total; the flush sums
+        them all); its i-th job in a launch takes the i-th range."""
+        if self._acc_map is not None and not self._acc_takes(jobs, device):
             acc_jobs, self._acc_flush, self._acc_map = self._acc_flush, None, None
             self._end_cycle(acc_jobs)
         if self._acc_map is None:
-            first = {}
-            for j in jobs:
+            plan = N.factor_accum_plan(jobs)
+            ranges, first = {}, {}
+            for j, (splits, nbytes) in zip(jobs, plan):
+                ranges.setdefault(j.F, []).append((splits, nbytes))
                 first.setdefault(j.F, j)
-            uniq = list(first.values())
-            plan = N.factor_accum_plan(uniq)
-            offs, total = [], 0
-            for _splits, nbytes in plan:
-                offs.append(total)
-                total += (nbytes + 255) // 256 * 256
+            total, offs = 0, {}
+            for F, rs in ranges.items():
+                offs[F] = total
+                total += sum(nb for _, nb in rs)  # (bytes are linear in the splits)
             buf = self._acc_buf
             if buf is None or buf.device != device or buf.numel() < total:
                 buf = self._acc_buf = torch.empty(total, dtype=torch.uint8, device=device)
             base = buf.data_ptr()
             self._acc_map, self._acc_live, flush = {}, set(), []
-            for j, (splits, _nbytes), off in zip(uniq, plan, offs):
-                self._acc_map[j.F] = (base + off, splits)
-                f = N.FactorJob.from_buffer_copy(j)
+            for F, rs in ranges.items():
+                starts, s0 = [], 0
+                for sp, _ in rs:
+                    starts.append((s0, sp))
+                    s0 += sp
+                self._acc_map[F] = (base + offs[F], starts, s0)
+                f = N.FactorJob.from_buffer_copy(first[F])
                 f.seg_ptrs, f.nseg = None, 0
-                f.acc, f.acc_splits = base + off, splits
+                f.acc, f.acc_splits, f.acc_stride = base + offs[F], s0, s0
                 f.alpha = 1.0  # partials already carry alpha; f.beta: 0 fresh factor, 1 existing
                 flush.append(f)
             self._acc_flush, self._acc_device = flush, device
+        seen = {}
         for j in jobs:
-            j.acc, j.acc_splits = self._acc_map[j.F]
-            j.acc_beta = 1.0 if j.F in self._acc_live else 0.0
-            self._acc_live.add(j.F)
+            k = seen.get(j.F, 0)
+            seen[j.F] = k + 1
+            acc, starts, stride = self._acc_map[j.F]
+            s0, sp = starts[k]
+            j.acc, j.acc_splits, j.acc_stride = acc + s0 * _SLAB_BYTES, sp, stride
+            j.acc_beta = 1.0 if (j.F, k) in self._acc_live else 0.0
+            self._acc_live.add((j.F, k))
 
     # ------------------------------------------------------------------ invert
     def _damping(self, add, multiply, count=None):

@@ -97,7 +97,15 @@ typedef struct kfac_factor_job {
    * an image fits the LDS-staged kernel; else one launch per batch).           */
   const void* seg_ptrs;
   int32_t nseg;
-  int32_t reserved2;
+  /* Deferred reduction, several jobs of one factor in ONE call (e.g. a pass's full
+   * batches as one multi-batch job and its short last batch as another): slabs per
+   * tile of the accumulator `acc` points into, 0 = acc_splits.  Each job owns its
+   * own slab range [s0, s0 + acc_splits) of an accumulator of acc_stride slabs per
+   * tile and passes acc = base + s0 * 64*64*sizeof(float) bytes (ranges must not
+   * overlap); kfac_factor_flush then takes acc = base, acc_splits = acc_stride =
+   * the total.  kfac_factor_accum_plan's bytes are linear in the splits, so the
+   * accumulator of such a factor is the sum of its jobs' planned bytes.          */
+  int32_t acc_stride;
 } kfac_factor_job;
 
 /* Workspace (split-K slabs) needed by kfac_factor_update for these jobs. */

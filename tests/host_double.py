@@ -9,6 +9,8 @@ import numpy as np
 
 
 UPDATES = []  # per kfac_factor_update call: nseg of each job
+ACC = {}      # deferred-reduction accumulators: slab-range pointer -> n x n partial sum
+SLAB_BYTES = 64 * 64 * 4  # a slab range starting at split s0 sits s0 tiles into the buffer
 
 
 def _view(ptr, count):
@@ -33,12 +35,12 @@ def fake_factor_update(jobs, device):
             X = np.concatenate([X, np.ones((X.shape[0], 1))], axis=1)
         n = op.cols + op.has_ones
         if j.acc:
+            # (modelled per slab range: ACC[acc pointer] = that range's n x n partial sum)
             assert j.acc_splits == 1
-            A = _view(j.acc, n * n).reshape(n, n)
             new = j.alpha * (X.T @ X)
             if j.acc_beta != 0.0:
-                new = new + j.acc_beta * A.astype(np.float64)
-            A[:] = new.astype(np.float32)
+                new = new + j.acc_beta * ACC[j.acc].astype(np.float64)
+            ACC[j.acc] = new.astype(np.float32)
             continue
         F = _view(j.F, n * j.ldF).reshape(n, j.ldF)
         new = j.alpha * (X.T @ X)
@@ -48,7 +50,11 @@ def fake_factor_update(jobs, device):
 
 
 def fake_accum_plan(jobs):
-    return [(1, (j.x.cols + j.x.has_ones) ** 2 * 4) for j in jobs]
+    # (one split; the device plan's bytes: lower-triangle tiles x splits x one 64 x 64 slab)
+    def tiles(n):
+        t = (n + 63) // 64
+        return t * (t + 1) // 2
+    return [(1, tiles(j.x.cols + j.x.has_ones) * SLAB_BYTES) for j in jobs]
 
 
 FLUSHES = []
@@ -59,7 +65,11 @@ def fake_factor_flush(jobs, device):
     FLUSHES.append(len(jobs))
     for j in jobs:
         n = j.x.cols + j.x.has_ones
-        A = _view(j.acc, n * n).reshape(n, n).astype(np.float64)
+        stride = j.acc_stride or j.acc_splits
+        used = [p for p in ACC if j.acc <= p < j.acc + stride * SLAB_BYTES]
+        A = sum(ACC[p].astype(np.float64) for p in used)
+        for p in used:  # (the cycle's ranges are consumed: the next cycle writes fresh ones)
+            del ACC[p]
         F = _view(j.F, n * j.ldF).reshape(n, j.ldF)
         new = j.alpha * A
         if j.beta != 0.0:

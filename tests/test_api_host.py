@@ -175,10 +175,11 @@ def test_queued_updates_merge_into_multibatch_jobs(monkeypatch):
                 torch.tensor(rng.standard_normal((B, 3)).astype(np.float32))]
                for B in sizes]
 
-    def run(defer_reduce, defer_batches=64, defer_bytes=256 << 20, launch_first=1):
+    def run(defer_reduce, defer_batches=64, defer_bytes=256 << 20, launch_first=1, merge=True):
         host_double.UPDATES.clear()
         net = mlp()
         kfac = KFAC(net)
+        kfac.merge_launches = merge
         kfac.defer_reduce, kfac.defer_batches = defer_reduce, defer_batches
         kfac.defer_bytes = defer_bytes
         kfac.launch_first = launch_first
@@ -200,8 +201,14 @@ def test_queued_updates_merge_into_multibatch_jobs(monkeypatch):
     for g, w in zip(got, want):
         np.testing.assert_allclose(g, w, rtol=1e-6)
     # a first launch of 16 queued updates: the whole pass is queued until the flush,
-    # one launch call per merge group: [8 8 8] [5] [8 8]
+    # one multi-batch job per merge group, all groups in ONE launch (each factor's
+    # three jobs on their own accumulator slab ranges): [8 8 8 | 5 | 8 8]
     got, launches = run(True, launch_first=16)
+    assert launches == [[3] * 4 + [1] * 4 + [2] * 4]
+    for g, w in zip(got, want):
+        np.testing.assert_allclose(g, w, rtol=1e-6)
+    # merge_launches off: one launch call per merge group
+    got, launches = run(True, launch_first=16, merge=False)
     assert launches == [[3] * 4, [1] * 4, [2] * 4]
     for g, w in zip(got, want):
         np.testing.assert_allclose(g, w, rtol=1e-6)

@@ -78,6 +78,12 @@ def main():
                            "ns_per_stage_p50": round(float(np.median(per)) * 1e3, 1),
                            "epilogue_us_p50": round(float(np.median(rt[sel, 3] - rt[sel, 2])), 2),
                            "prologue_us_p50": round(float(np.median(rt[sel, 1] - rt[sel, 0])), 2)}
+    narrow = ~full
+    if narrow.any():
+        out["narrow_end_us_p50_p100"] = np.percentile(rt[narrow, 3], [50, 100]).round(2).tolist()
+    for m in sorted(set(mask[full].tolist())):
+        sel = full & (mask == m)
+        out[f"mask{m}"]["end_us_p50_p100"] = np.percentile(rt[sel, 3], [50, 100]).round(2).tolist()
     # per-SIMD load: HW_ID bits (gfx9): wave 3:0, simd 5:4, cu 11:8, sh 12, se 15:13
     hw = s[:, 6]
     simd = (s[:, 7] & 0xFF) * 10000 + ((hw >> 13) & 7) * 1000 + ((hw >> 12) & 1) * 100 + ((hw >> 8) & 15) * 10 + ((hw >> 4) & 3)
