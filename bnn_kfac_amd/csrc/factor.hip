@@ -752,10 +752,10 @@ constexpr int X3_THREADS = 128;
 // edge: the lower-triangle tiles, or with a thin last tile row (T >= 2 and at most 32
 // rows in it) the T-1 pairs (i, i) + (T-1, i), the other strictly lower tiles of rows
 // < T-1 and the corner (see X3_PAIR)
-static bool x3_merge() {  // KFAC_X3_TAIL=0: tail jobs ordered and planned like the others (A/B)
+static bool x3_merge() {  // KFAC_X3_TAIL=1: tail jobs last, outside the dispatch-round plan (A/B)
   static const bool on = [] {
     const char* v = getenv("KFAC_X3_TAIL");
-    return v ? atoi(v) != 0 : true;
+    return v ? atoi(v) != 0 : false;
   }();
   return on;
 }

@@ -434,7 +434,9 @@ def test_conv_multibatch_queue_vs_oracle(hip_device, spec, deferred):
     finally:
         N.factor_update = orig
     if deferred:
-        assert calls[0] == [7, 7], calls  # the 7 equal batches: one job per factor
+        # the 7 equal batches: one job per factor (the short batch's jobs follow in the
+        # same launch when merge_launches holds, else in a launch of their own)
+        assert calls[0][:2] == [7, 7], calls
     wA = sum(O.conv_factor_A(x, k, p, s, bias, np.float64) for x in xs)
     wG = sum(O.grad_factor(g, np.float64) for g in gs)
     np.testing.assert_allclose(A.cpu().numpy(), wA, **FT)
