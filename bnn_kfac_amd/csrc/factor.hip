@@ -2058,13 +2058,12 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
   }
   // workgroups of job i at `splits` K-splits
   auto job_tasks = [&](int i, int64_t splits) { return units[i] * splits; };
-  // kfac_factor_tiles_x3: a narrow job (n <= 32, one fp32-MFMA tile, latency-bound
-  // direct loads) takes X3_NARROW_SPLIT times the K-splits of the chunk, so its few
-  // tasks end well before the bf16x3 tiles' (MNIST MLP G2: ~230 us of a 270 us launch
-  // at the common chunk)
+  // kfac_factor_tiles_x3: KFAC_X3_NARROW=f gives a narrow job (n <= 32, one fp32-MFMA
+  // tile) f times the K-splits of the chunk, so its few tasks end earlier; f = 4 measured
+  // ~1 % slower on the MLP line than the default 1 (profiles/r04ah/)
   static const int64_t narrow_f = [] {
     const char* v = getenv("KFAC_X3_NARROW");
-    return (int64_t)(v ? std::max(1, atoi(v)) : 4);
+    return (int64_t)(v ? std::max(1, atoi(v)) : 1);
   }();
   auto job_splits = [&](int i, int64_t c) {
     const int64_t st = job_stages(jobs[i]);
