@@ -339,15 +339,34 @@ def test_queued_pass_matches_per_batch_launches(hip_device):
     recs = [(torch.rand(B, 784, device=hip_device, generator=g), torch.rand(B, 128, device=hip_device, generator=g),
              torch.randn(B, 128, device=hip_device, generator=g), torch.randn(B, 10, device=hip_device, generator=g))
             for B in (4096,) * 6 + (1700,)]
+    from bnn_kfac_amd import _native as N
     outs = []
-    for defer_batches in (1, 64, 4):
+    orig = N.factor_update
+    # (defer_batches, launch_first, merge_launches): per update; doubling launches; the
+    # whole pass queued as one flush of two groups (6 full batches, 1 short) in two
+    # launches, or in ONE launch whose jobs own separate split-K slab ranges (acc_stride)
+    for defer_batches, first, merge in ((1, 1, False), (64, 1, False), (4, 1, False), (64, 16, False),
+                                        (64, 16, True)):
         kfac = KFAC(net)
         kfac.defer_batches = defer_batches
-        for a1, a2, g1, g2 in recs:
-            kfac.record[net[0]] = [a1, g1]
-            kfac.record[net[2]] = [a2, g2]
-            kfac.update(a1.shape[0])
-        outs.append([t.cpu().numpy() for pair in kfac.state.values() for t in pair])
+        kfac.launch_first = first
+        kfac.merge_launches = merge
+        calls = []
+
+        def counting(jobs, device):
+            calls.append(len(jobs))
+            return orig(jobs, device)
+        N.factor_update = counting
+        try:
+            for a1, a2, g1, g2 in recs:
+                kfac.record[net[0]] = [a1, g1]
+                kfac.record[net[2]] = [a2, g2]
+                kfac.update(a1.shape[0])
+            outs.append([t.cpu().numpy() for pair in kfac.state.values() for t in pair])
+        finally:
+            N.factor_update = orig
+        if first == 16:
+            assert calls == ([8] if merge else [4, 4]), calls
     for other in outs[1:]:
         for got, want in zip(other, outs[0]):
             np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-6 * np.abs(want).max())
