@@ -155,6 +155,8 @@ _SLAB_BYTES = 64 * 64 * 4
 # A/B: KFAC_SKIP_DONE_WAITS=0 keeps a stream wait on events the host has seen complete
 _SKIP_DONE_WAITS = os.environ.get("KFAC_SKIP_DONE_WAITS", "1") != "0"
 _MERGE_LAUNCHES = os.environ.get("KFAC_MERGE_LAUNCHES", "0") == "1"
+# stream priority of the inversion side streams (-1 high, 0 normal; A/B knob)
+_INV_STREAM_PRIO = int(os.environ.get("KFAC_INV_STREAM_PRIO", "-1"))
 
 
 def _same_shapes(f, g):
@@ -839,7 +841,7 @@ class KFAC(Curvature):
         chip (wide MLP: 13.8 -> 25.5 ms per inversion when they did)."""
         s = self._inv_streams.get(device.index)
         if s is None:
-            s = self._inv_streams[device.index] = [torch.cuda.Stream(device=device, priority=-1)
+            s = self._inv_streams[device.index] = [torch.cuda.Stream(device=device, priority=_INV_STREAM_PRIO)
                                                    for _ in range(2)]
         if not isinstance(s, list):  # a single stream set by hand (tools/probe_*.py)
             return s
