@@ -235,6 +235,47 @@ def test_deferred_reduce_raw_abi(hip_device):
     np.testing.assert_array_equal(F.cpu().numpy(), want)
 
 
+def test_split_accumulator_ranges_raw_abi(hip_device):
+    """Two jobs of ONE factor in ONE kfac_factor_update call, each accumulating into its
+    own split-K slab range (acc = base + s0 slabs, acc_stride = the factor's total), then
+    one kfac_factor_flush over all slabs (include/kfac_hip.h, acc_stride): F0 + both
+    batches, exact on small integers, for the fp32-MFMA (129) and bf16x3 (785) kernels.
+    An acc_stride below acc_splits is rejected before any launch."""
+    from bnn_kfac_amd import _native as N
+    rng = np.random.default_rng(11)
+    slab = 64 * 64 * 4
+    for cols in (128, 784):
+        n = cols + 1
+        F0 = rng.integers(-4, 5, size=(n, n)).astype(np.float32)
+        F0 = F0 + F0.T
+        F = _t(F0, hip_device)
+        xs = [rng.integers(-3, 4, size=(B, cols)).astype(np.float32) for B in (4096, 608)]
+        xd = [_t(x, hip_device) for x in xs]
+        jobs = [N.factor_job(N.rowmajor_operand(x, True), F, 1.0, 1.0) for x in xd]
+        plan = N.factor_accum_plan(jobs)
+        total = sum(sp for sp, _ in plan)
+        acc = torch.empty(sum(nb for _, nb in plan), dtype=torch.uint8, device=hip_device)
+        s0 = 0
+        for j, (sp, _) in zip(jobs, plan):
+            j.acc, j.acc_splits, j.acc_beta, j.acc_stride = acc.data_ptr() + s0 * slab, sp, 0.0, total
+            s0 += sp
+        bad = N.FactorJob.from_buffer_copy(jobs[0])
+        bad.acc_stride = max(1, bad.acc_splits - 1) if bad.acc_splits > 1 else -1
+        with pytest.raises(N.NativeError):
+            N.factor_update([bad], hip_device)
+        N.factor_update(jobs, hip_device)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(F.cpu().numpy(), F0)
+        f = N.factor_job(N.rowmajor_operand(xd[0], True), F, 1.0, 1.0)
+        f.acc, f.acc_splits, f.acc_stride = acc.data_ptr(), total, total
+        N.factor_flush([f], hip_device)
+        want = F0.astype(np.float64)
+        for x in xs:
+            xo = np.concatenate([x, np.ones((x.shape[0], 1), np.float32)], 1).astype(np.float64)
+            want += xo.T @ xo
+        np.testing.assert_array_equal(F.cpu().numpy(), want)
+
+
 @pytest.mark.parametrize("cols,rows,offset,ones", [(784, 4096, 0, True), (128, 1000, 0, False),
                                                     (129, 333, 0, True), (10, 4096, 0, False),
                                                     (96, 777, 1, True), (31, 65, 0, True)])
