@@ -41,6 +41,8 @@ struct FactorJobDev {
   char* split3;      // pre-split bf16x3 panel images of the job (kfac_factor_syrk3), else null
   int x3pair;        // kfac_factor_tiles_x3: thin last tile row, diagonal + edge tiles paired
   int sstride;       // slabs per tile of `slab` (a job's split s of tile t: t * sstride + s)
+  int xsplits;       // x3 thin-row pairs: of the `splits` slabs per tile, the last xsplits are
+                     // written by extra, shorter K-splits of the pair units only (x3_xsplits)
 };
 
 struct FactorArgs {
@@ -767,6 +769,18 @@ static bool x3_pairing() {  // KFAC_X3_PAIR=0: no pairs (A/B)
   return on;
 }
 static inline bool x3_thin(int n, int T) { return x3_pairing() && T >= 2 && n - TILE * (T - 1) <= 32; }
+// KFAC_X3_PAIR_XS=k: a thin-row x3 job with f full-tile K-splits gets S = f + f / k slabs
+// per tile, the last f / k of them written by extra K-splits of its pair units only
+// (0: none, the A/B)
+static int x3_pair_xs() {
+  static const int k = [] {
+    const char* v = getenv("KFAC_X3_PAIR_XS");
+    return v ? std::max(0, atoi(v)) : 10;
+  }();
+  return k;
+}
+// S / (k + 1) recovers f / k from S = f + f / k (f = k a + b, b <= k - 1)
+static inline int64_t x3_xsplits(int64_t S) { return x3_pair_xs() ? S / (x3_pair_xs() + 1) : 0; }
 __host__ __device__ inline int x3_units_of(int T, bool pair) { return T * (T + 1) / 2 - (pair ? T - 1 : 0); }
 static inline int x3_units(int n, int T) { return x3_units_of(T, x3_thin(n, T)); }
 constexpr int X3_NW = X3_THREADS / 64;
@@ -1079,8 +1093,16 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
   const int T = J.t;
   const bool thin = J.x3pair != 0;
   const int units = x3_units_of(T, thin);
-  const int split = split_major ? local / units : local % J.splits;
-  const int unit = split_major ? local - split * units : local / J.splits;
+  const int sf = J.splits - J.xsplits;  // the full K-splits (every unit)
+  int split, unit;
+  if (local >= units * sf) {  // the pair units' extra K-splits (x3_xsplits)
+    const int e = local - units * sf;
+    split = sf + e / (T - 1);
+    unit = e - (split - sf) * (T - 1);
+  } else {
+    split = split_major ? local / units : local % sf;
+    unit = split_major ? local - split * units : local / sf;
+  }
   int ti, tj;
   bool pair = false;
   if (!thin) {
@@ -1096,8 +1118,10 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
     ti = tj = T - 1;
   }
   const int tile = ti * (ti + 1) / 2 + (pair ? ti : tj);  // (a pair's: its diagonal tile)
-  const int64_t s0 = (int64_t)split * J.chunk;
-  const int64_t s1 = min(J.nst, s0 + J.chunk);
+  // a pair unit's K-chunk: nst over all `splits` slabs; the others' over the full splits
+  const int64_t chunk = pair && J.xsplits ? (J.nst + J.splits - 1) / J.splits : J.chunk;
+  const int64_t s0 = (int64_t)split * chunk;
+  const int64_t s1 = min(J.nst, s0 + chunk);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool same = ti == tj;
@@ -1210,6 +1234,16 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
         for (int v = 0; v < 16; ++v) acc[bi][bj][v] += xo[(((1 - wave) * 2 + bj) * 16 + v) * 64 + lane];
         put_partial(J, acc[bi][bj],
                     [&](int v) { return &out[(bi * 32 + acc_row(v, lane)) * TILE + bj * 32 + (lane & 31)]; });
+        // the slabs of the pair units' extra K-splits hold nothing of this tile: its
+        // last full K-split writes them as zero partials
+        if (split == sf - 1)
+          for (int x = 1; x <= J.xsplits; ++x) {
+            floatx16 z;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) z[v] = 0.f;
+            float* o = out + (size_t)x * TILE * TILE;
+            put_partial(J, z, [&](int v) { return &o[(bi * 32 + acc_row(v, lane)) * TILE + bj * 32 + (lane & 31)]; });
+          }
       }
   };
   if (wave == 0) hand(std::integral_constant<int, 1>{});
@@ -1923,7 +1957,8 @@ __global__ __launch_bounds__(NTHREADS) void kfac_factor_reduce(FactorArgs args) 
 
 // ------------------------------------------------------------------- host side
 struct Plan {
-  int tiles, splits;
+  int tiles, splits;  // splits: slabs per tile (x3 thin jobs: splits - xsplits full K-splits)
+  int xsplits;
   int units;  // workgroups per K-split: tiles, or a staged conv job's block groups
   int tasks;  // workgroups of the job
   int64_t chunk;
@@ -2056,8 +2091,19 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
     else if (x3) units[i] = x3_units((int)factor_n(jobs[i]), (int)t);
     else units[i] = conv_geom(jobs[i], cg) ? cg.units : t * (t + 1) / 2;
   }
-  // workgroups of job i at `splits` K-splits
-  auto job_tasks = [&](int i, int64_t splits) { return units[i] * splits; };
+  // x3 jobs with thin-row pairs: the pair units are the slowest (30 MFMAs on 3
+  // fragments per 16 rows: 1,577 vs 1,423 ns per stage for a full tile, profiles/r04ae/),
+  // so they take S/11 more K-splits (x3_xsplits) and end with the full tiles
+  auto xs_of = [&](int i, int64_t S) {
+    const int t = (int)cdiv(factor_n(jobs[i]), TILE);
+    return x3 && x3_thin(factor_n(jobs[i]), t) ? x3_xsplits(S) : 0;
+  };
+  // workgroups of job i at `splits` slabs per tile
+  auto job_tasks = [&](int i, int64_t splits) {
+    const int64_t xs = xs_of(i, splits);
+    const int t = (int)cdiv(factor_n(jobs[i]), TILE);
+    return units[i] * (splits - xs) + (int64_t)(t - 1) * xs * (xs > 0);
+  };
   // kfac_factor_tiles_x3: KFAC_X3_NARROW=f gives a narrow job (n <= 32, one fp32-MFMA
   // tile) f times the K-splits of the chunk, so its few tasks end earlier; f = 4 measured
   // ~1 % slower on the MLP line than the default 1 (profiles/r04ah/)
@@ -2068,7 +2114,10 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
   auto job_splits = [&](int i, int64_t c) {
     const int64_t st = job_stages(jobs[i]);
     const int64_t sp = cdiv(st, c);
-    return x3 && factor_n(jobs[i]) <= 32 ? std::min(st, sp * narrow_f) : sp;
+    if (x3 && factor_n(jobs[i]) <= 32) return std::min(st, sp * narrow_f);
+    const int t = (int)cdiv(factor_n(jobs[i]), TILE);
+    if (x3 && x3_thin(factor_n(jobs[i]), t) && x3_pair_xs()) return std::min(st, sp + sp / x3_pair_xs());
+    return sp;
   };
   auto tasks_at = [&](int64_t c) {
     int64_t n = 0;
@@ -2103,7 +2152,8 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
     const int64_t steps = job_stages(jobs[i]);
     if (jobs[i].acc) {
       p.splits = jobs[i].acc_splits;
-      p.chunk = cdiv(steps, (int64_t)p.splits);
+      p.xsplits = (int)xs_of(i, p.splits);
+      p.chunk = cdiv(steps, (int64_t)(p.splits - p.xsplits));
       p.slab_bytes = 0;  // partials go to the caller's accumulator
       p.tasks = (int)job_tasks(i, p.splits);
       continue;
@@ -2137,7 +2187,8 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
       k = std::min(k, cg.B);
       p.splits = (int)cdiv(cg.B, k);
     }
-    p.chunk = cdiv(steps, (int64_t)p.splits);
+    p.xsplits = (int)xs_of(i, p.splits);
+    p.chunk = cdiv(steps, (int64_t)(p.splits - p.xsplits));
     p.slab_bytes = align_up((size_t)p.tiles * p.splits * TILE * TILE * sizeof(float), 256);
     p.tasks = (int)job_tasks(i, p.splits);
   }
@@ -2235,6 +2286,7 @@ static int prepare_group(const kfac_factor_job* jobs_in, int njobs, char* ws, si
     d.glds = job_glds(jb);
     d.x3pair = tiles_x3_group(jobs, njobs) && x3_thin(d.n, d.t);
     d.splits = plans[i].splits;
+    d.xsplits = plans[i].xsplits;
     d.sstride = jb.acc && jb.acc_stride > 0 ? jb.acc_stride : d.splits;
     d.chunk = plans[i].chunk;
     if (d.nseg > 1) {  // kfac_factor_update keeps a launch within KSEG batch bases

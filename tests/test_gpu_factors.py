@@ -370,6 +370,53 @@ def test_x3_thin_row_pairs_exact(hip_device, deferred):
         np.testing.assert_array_equal(F.cpu().numpy(), w)
 
 
+@pytest.mark.parametrize("deferred", [False, True])
+def test_x3_pair_extra_splits_exact(hip_device, deferred):
+    """Thin-row pair units take S/11 extra, shorter K-splits of S slabs per tile (the
+    full tiles' last K-split writes zero partials into those slabs): a 785 factor (pairs)
+    beside a 128 one (no pairs) over 8 batches of 4096 rows, planned at S >= 11, exact on
+    small integers against the fp64 sum, immediate and deferred."""
+    from bnn_kfac_amd import _native as N
+    rng = np.random.default_rng(13)
+    nseg, rows = 8, 4096
+    jobs, want, keep, outs, accs = [], [], [], [], []
+    for cols, ones in ((784, True), (128, False)):
+        xs = [rng.integers(-2, 3, size=(rows, cols)).astype(np.float32) for _ in range(nseg)]
+        views = [_t(x, hip_device) for x in xs]
+        keep.append(views)
+        n = cols + ones
+        F = torch.full((n, n), np.nan, device=hip_device)
+        outs.append(F)
+        table = N.segment_table([v.data_ptr() for v in views])
+        keep.append(table)
+        job = N.factor_job(N.rowmajor_operand(views[0], ones), F, 1.0, 0.0)
+        job.seg_ptrs, job.nseg = N.table_ptr(table), nseg
+        jobs.append(job)
+        w = np.zeros((n, n))
+        for x in xs:
+            xo = np.concatenate([x, np.ones((rows, 1), np.float32)], 1) if ones else x
+            w += xo.T.astype(np.float64) @ xo
+        want.append(w)
+    plan = N.factor_accum_plan(jobs)
+    assert plan[0][0] >= 11, plan  # the 785 factor's pair units get extra K-splits
+    if deferred:
+        flush = []
+        for job, (splits, nbytes) in zip(jobs, plan):
+            acc = torch.empty(nbytes, dtype=torch.uint8, device=hip_device)
+            accs.append(acc)
+            job.acc, job.acc_splits, job.acc_beta = acc.data_ptr(), splits, 0.0
+            f = N.FactorJob.from_buffer_copy(job)
+            f.seg_ptrs, f.nseg = None, 0
+            flush.append(f)
+        N.factor_update(jobs, hip_device)
+        N.factor_flush(flush, hip_device)
+    else:
+        N.factor_update(jobs, hip_device)
+    torch.cuda.synchronize()
+    for F, w in zip(outs, want):
+        np.testing.assert_array_equal(F.cpu().numpy(), w)
+
+
 def test_queued_pass_matches_per_batch_launches(hip_device):
     """KFAC's default queued pass (multi-batch jobs, one short last batch, separate
     record allocations) equals launching every update on its own."""
