@@ -775,7 +775,7 @@ static inline bool x3_thin(int n, int T) { return x3_pairing() && T >= 2 && n - 
 static int x3_pair_xs() {
   static const int k = [] {
     const char* v = getenv("KFAC_X3_PAIR_XS");
-    return v ? std::max(0, atoi(v)) : 10;
+    return v ? std::max(0, atoi(v)) : 5;
   }();
   return k;
 }
@@ -2092,8 +2092,8 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
     else units[i] = conv_geom(jobs[i], cg) ? cg.units : t * (t + 1) / 2;
   }
   // x3 jobs with thin-row pairs: the pair units are the slowest (30 MFMAs on 3
-  // fragments per 16 rows: 1,577 vs 1,423 ns per stage for a full tile, profiles/r04ae/),
-  // so they take S/11 more K-splits (x3_xsplits) and end with the full tiles
+  // fragments per 16 rows: 1,606 vs 1,434 ns per stage for a full tile, profiles/r04am/),
+  // so they take f/k more K-splits (x3_xsplits) and end with the full tiles
   auto xs_of = [&](int i, int64_t S) {
     const int t = (int)cdiv(factor_n(jobs[i]), TILE);
     return x3 && x3_thin(factor_n(jobs[i]), t) ? x3_xsplits(S) : 0;
