@@ -312,12 +312,10 @@ def invert(jobs, device: torch.device, inputs_read=None) -> torch.Tensor:
     need = L.kfac_invert_workspace_bytes(arr, len(jobs))
     stream = stream_handle(device)
     ws = workspace.get(device, need, stream)
-    # zeroed by kfac_invert; one buffer per (device, stream, size): stream order makes
-    # the reuse safe (its readback is queued on the same stream before the next write)
-    key = (device.index, stream, len(jobs))
-    info = _info_bufs.get(key)
-    if info is None:
-        info = _info_bufs[key] = torch.empty(len(jobs), dtype=torch.int32, device=device)
+    # a fresh verdict tensor per call (zeroed by kfac_invert): callers may hold several
+    # calls' verdicts at once (the pooled buffer is only invert_pipelined's, whose
+    # verdict is copied to host on the same stream before the buffer is written again)
+    info = torch.empty(len(jobs), dtype=torch.int32, device=device)
     ev = None
     if inputs_read is not None:
         ev = inputs_read.cuda_event
@@ -330,7 +328,9 @@ def invert_pipelined(jobs, device: torch.device, info_host: torch.Tensor, order:
                      inputs_read, done: "RawEvent", main: int, side: int, side_stream=None) -> torch.Tensor:
     """kfac_invert_pipelined: `side` ordered after `main`, the grouped inversion on `side`
     (`inputs_read` recorded after the F-reading launch), the verdict copied into the
-    pinned `info_host`, `done` recorded on `side`.  Returns the device verdict vector."""
+    pinned `info_host`, `done` recorded on `side`.  Returns the device verdict vector:
+    a buffer pooled per (device, side stream, job count) that the next such call on
+    that stream overwrites -- read `info_host` (after `done`), or clone it first."""
     L = lib()
     arr = as_array(InvertJob, jobs)
     need = L.kfac_invert_workspace_bytes(arr, len(jobs))

@@ -48,16 +48,9 @@ struct FactorJobDev {
 struct FactorArgs {
   const float* segs[KSEG];  // batch bases of the multi-batch jobs (kernel arguments: no copy)
   int njobs;
-  int stagger;  // start delay per dispatch round, in 512-cycle s_sleep(8) units
   int split_major;  // LDS-DMA path task order: 1 split-major, 0 tile-major (KFAC_SYRK_ORDER)
   int task_end[MAXJ];
   int tile_end[MAXJ];
-  // kfac_factor_tiles_x3, jobs of equal splits: the tasks of ONE split of every job
-  // are contiguous (unit_end: prefix sums of the jobs' units), so xcd_task hands each
-  // XCD whole K-ranges of all factors (KFAC_X3_INTERLEAVE)
-  int interleave;
-  int unit_end[MAXJ];
-  int main_tasks;  // kfac_factor_tiles_x3: tasks before the tail jobs' (XCD-mapped), the rest in dispatch order
   FactorJobDev job[MAXJ];
 };
 
@@ -429,6 +422,9 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, const fl
 // path (or the narrow direct-load path), and the ring is all the LDS (32 KB, not the
 // register-staged path's 34 KB): 4 resident workgroups leave 32 KB of a CU's 160,
 // room for a 32-tile inversion workgroup (29 KB) of an overlapped invert().
+// start delay per dispatch round (blockIdx / 256), in 512-cycle s_sleep(8) units
+constexpr int STAGGER = 5;
+
 template <int GBK, int NSLOT, bool GLDS_ONLY = false, int FAMILY = KFAC_ROWMAJOR>
 __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs args) {
   constexpr int RING = FAMILY == KFAC_ROWMAJOR ? NSLOT * 2 * GBK * TILE : 0;
@@ -437,7 +433,7 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
   // Workgroups of later dispatch rounds (blockIdx / 256: the ~4 sharing a CU) start a
   // fraction of a stage later, so their DMA waits and barriers interleave instead of
   // stalling all 16 waves of a CU together (measured +2.5% on the MLP update).
-  for (int i = 0; i < args.stagger * (int)(blockIdx.x >> 8); ++i) __builtin_amdgcn_s_sleep(8);
+  for (int i = 0; i < STAGGER * (int)(blockIdx.x >> 8); ++i) __builtin_amdgcn_s_sleep(8);
   const int task = xcd_task(blockIdx.x, gridDim.x);
   int j = 0;
   while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
@@ -754,13 +750,6 @@ constexpr int X3_THREADS = 128;
 // edge: the lower-triangle tiles, or with a thin last tile row (T >= 2 and at most 32
 // rows in it) the T-1 pairs (i, i) + (T-1, i), the other strictly lower tiles of rows
 // < T-1 and the corner (see X3_PAIR)
-static bool x3_merge() {  // KFAC_X3_TAIL=1: tail jobs last, outside the dispatch-round plan (A/B)
-  static const bool on = [] {
-    const char* v = getenv("KFAC_X3_TAIL");
-    return v ? atoi(v) != 0 : false;
-  }();
-  return on;
-}
 static bool x3_pairing() {  // KFAC_X3_PAIR=0: no pairs (A/B)
   static const bool on = [] {
     const char* v = getenv("KFAC_X3_PAIR");
@@ -856,9 +845,6 @@ __device__ __forceinline__ X3Frag x3_split8(const float (&x)[8]) {
 // the buffer's record limit (0), and the ones column (FILL: only the tasks whose
 // fragments hold it) is a select of 1 / 0 by row validity.
 // Microbench: tools/microbench/x3w_mb.hip; DESIGN.md §3.1c.
-#ifndef KFAC_X3_AB
-#define KFAC_X3_AB 0  // timing A/B builds (tools/build_ab.sh): 1 no reloads, 2 no split, 3 neither
-#endif
 struct X3Cursor {  // a stage to load: batch `seg` (base `b`), first row `k`
   const float* b;
   int seg, k;
@@ -956,25 +942,8 @@ __device__ __forceinline__ void x3_loop(const FactorJobDev& J, const float* cons
   // split fragment f (of the stage starting at row kstage) and reload its registers
   auto take = [&](int f, int kstage, const X3Cursor& c) {
     fix(f, kstage);
-#if KFAC_X3_AB == 2 || KFAC_X3_AB == 3  // timing A/B only: hi parts only (4 VALU, bf16 products)
-    X3Frag fr;
-    typedef uint32_t u32x4_ab __attribute__((ext_vector_type(4)));
-    u32x4_ab h;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) h[i] = bf16_pair(x[f][2 * i], x[f][2 * i + 1]);
-    const u32x4_ab z = {0u, 0u, 0u, 0u};
-    fr.p[0] = __builtin_bit_cast(bf16x8, h);
-    fr.p[1] = __builtin_bit_cast(bf16x8, z);
-    fr.p[2] = __builtin_bit_cast(bf16x8, z);
-#else
     const X3Frag fr = x3_split8(x[f]);
-#endif
-#if KFAC_X3_AB != 1 && KFAC_X3_AB != 3  // (1, 3: timing A/B only: no reloads)
     ld8(f, c, x[f]);
-#else
-#pragma unroll
-    for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(x[f][r]));  // (no hoisting of the split)
-#endif
     return fr;
   };
   X3Frag pa = take(0, k0, c2);
@@ -1073,19 +1042,6 @@ __device__ __forceinline__ void x3_loop(const FactorJobDev& J, const float* cons
   }
 }
 
-#ifndef KFAC_X3_STAMPS
-#define KFAC_X3_STAMPS 0  // diagnostic builds only: per-workgroup timeline of the x3 launch
-#endif
-#if KFAC_X3_STAMPS
-// [block][8]: realtime at start / loop start / loop end / end, shader clocks at loop
-// start / end, HW_ID, XCC_ID | mask << 8 | stages << 16 (tools/x3_stamps.py)
-__device__ unsigned long long g_x3_stamps[8192 * 8];
-#define X3_STAMP(i, v) \
-  if (threadIdx.x == 0 && blockIdx.x < 8192) g_x3_stamps[blockIdx.x * 8 + (i)] = (unsigned long long)(v)
-#else
-#define X3_STAMP(i, v)
-#endif
-
 template <int GBK, int NSLOT>
 __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const float* const* segs, int local,
                                                float* lds, int split_major) {
@@ -1144,9 +1100,6 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
       for (int v = 0; v < 16; ++v) acc[bi][bj][v] = 0.f;
 #pragma unroll
   for (int v = 0; v < 16; ++v) acc4[v] = 0.f;
-  X3_STAMP(1, wall_clock64());
-  X3_STAMP(4, __builtin_amdgcn_s_memtime());
-  X3_STAMP(7, (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) | (mask << 8) | ((uint32_t)(s1 - s0) << 16));
   if (s1 > s0) {
     // FILL: one of the task's fragments holds the ones column (the last tile row /
     // column of an A factor with a bias)
@@ -1167,8 +1120,6 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
     }
 #undef X3_CASE
   }
-  X3_STAMP(2, wall_clock64());
-  X3_STAMP(5, __builtin_amdgcn_s_memtime());
   if (pair) {
     // wave 0 keeps D00, E00, E01 and wave 1 D10, D11; each hands the other's through
     // LDS slots [D00, D10, D11, E00, E01][16 values][64 lanes]; sums are w0 + w1
@@ -1259,37 +1210,18 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
 __global__ __launch_bounds__(X3_THREADS, 2) void kfac_factor_tiles_x3(FactorArgs args) {
   // (LDS only for the epilogue's hand-off: a block row, 16 KB; a pair's blocks, 20 KB)
   __shared__ __attribute__((aligned(16))) float lds[5 * 16 * 64];
-  X3_STAMP(0, wall_clock64());
-  X3_STAMP(6, (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4));
-  X3_STAMP(7, 0);  // (narrow tasks leave it 0; x3 tasks overwrite it)
-  for (int i = 0; i < args.stagger * (int)(blockIdx.x >> 8); ++i) __builtin_amdgcn_s_sleep(8);
-  // the main jobs' tasks XCD-contiguous (xcd_task), the tail jobs' in dispatch order:
-  // they start as the main tasks end, on every XCD
-  const int task = (int)blockIdx.x < args.main_tasks ? xcd_task(blockIdx.x, args.main_tasks) : (int)blockIdx.x;
-  int j = 0, local;
-  if (args.interleave) {  // task = split * U + unit of the concatenated jobs' units
-    const int U = args.unit_end[args.njobs - 1];
-    const int sp = task / U, u = task - sp * U;
-    while (j + 1 < args.njobs && u >= args.unit_end[j]) ++j;
-    const int ub = j ? args.unit_end[j - 1] : 0;
-    local = sp * (args.unit_end[j] - ub) + (u - ub);  // (split-major local order)
-  } else {
-    while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
-    local = task - args.job[j].task_begin;
-  }
+  for (int i = 0; i < STAGGER * (int)(blockIdx.x >> 8); ++i) __builtin_amdgcn_s_sleep(8);
+  const int task = xcd_task(blockIdx.x, gridDim.x);
+  int j = 0;
+  while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
+  const int local = task - args.job[j].task_begin;
   const FactorJobDev& J = args.job[j];
   if (J.n <= 32)
     factor_task_narrow_direct<X3_NW>(J, args.segs, local, lds);
   else
     factor_task_x3<BK, 2>(J, args.segs, local, lds, args.split_major);
-  X3_STAMP(3, wall_clock64());
 }
 
-#if KFAC_X3_STAMPS
-extern "C" __attribute__((visibility("default"))) int kfac_debug_x3_stamps(void* host, size_t bytes) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_x3_stamps), std::min(bytes, sizeof(g_x3_stamps))) == hipSuccess ? 0 : -1;
-}
-#endif
 
 // ------------------------------------------------------------ conv operands
 // Conv2d factors with each image staged whole in LDS (replaces the per-element
@@ -2058,26 +1990,12 @@ static bool tiles_x3_group(const kfac_factor_job* jobs, int njobs) {
   return nmax >= (tiles_x3_mode() == 1 ? 33 : 512);
 }
 
-// A tail job of a kfac_factor_tiles_x3 group: fewer than half the stages of the
-// group's largest job (a pass's short last batch beside its multi-batch full batches).
-// Its tasks are dispatched after the others' and are not counted against the slots.
-static bool x3_tail(const kfac_factor_job* jobs, int njobs, int i, bool x3) {
-  if (!x3 || !x3_merge()) return false;
-  int64_t mx = 0;
-  for (int k = 0; k < njobs; ++k) mx = std::max(mx, job_stages(jobs[k]));
-  return 2 * job_stages(jobs[i]) < mx;
-}
-
 static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
                       int64_t slots = 0) {
   const bool s3 = syrk3_group(jobs, njobs);
   // resident workgroups per CU: 4 (32 KB of LDS each; kfac_factor_tiles_x3: 4 of two
   // waves -- 3 or 2 measured slower); the bf16x3 kernel: S3D_WGS (49 KB each)
-  static const int env_wgs = [] {  // (tuning experiments: resident workgroups per CU planned for)
-    const char* v = getenv("KFAC_SYRK_WGS");
-    return v ? atoi(v) : 0;
-  }();
-  if (slots <= 0) slots = (env_wgs > 0 ? env_wgs : (s3 ? S3D_WGS : 4)) * 256;
+  if (slots <= 0) slots = (s3 ? S3D_WGS : 4) * 256;
   constexpr int64_t MIN_CHUNK = 8, OVERHEAD = 4;  // stages; ~per-task fixed cost in stages
   int64_t max_steps = 1;
   for (int i = 0; i < njobs; ++i) max_steps = std::max(max_steps, job_stages(jobs[i]));
@@ -2104,17 +2022,11 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
     const int t = (int)cdiv(factor_n(jobs[i]), TILE);
     return units[i] * (splits - xs) + (int64_t)(t - 1) * xs * (xs > 0);
   };
-  // kfac_factor_tiles_x3: KFAC_X3_NARROW=f gives a narrow job (n <= 32, one fp32-MFMA
-  // tile) f times the K-splits of the chunk, so its few tasks end earlier; f = 4 measured
-  // ~1 % slower on the MLP line than the default 1 (profiles/r04ah/)
-  static const int64_t narrow_f = [] {
-    const char* v = getenv("KFAC_X3_NARROW");
-    return (int64_t)(v ? std::max(1, atoi(v)) : 1);
-  }();
+  // (kfac_factor_tiles_x3: narrow jobs (n <= 32) at 4x the chunk's K-splits measured ~1 %
+  // slower on the MLP line, profiles/r04ah/)
   auto job_splits = [&](int i, int64_t c) {
     const int64_t st = job_stages(jobs[i]);
     const int64_t sp = cdiv(st, c);
-    if (x3 && factor_n(jobs[i]) <= 32) return std::min(st, sp * narrow_f);
     const int t = (int)cdiv(factor_n(jobs[i]), TILE);
     if (x3 && x3_thin(factor_n(jobs[i]), t) && x3_pair_xs()) return std::min(st, sp + sp / x3_pair_xs());
     return sp;
@@ -2122,19 +2034,15 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
   auto tasks_at = [&](int64_t c) {
     int64_t n = 0;
     for (int i = 0; i < njobs; ++i)
-      if (!x3_tail(jobs, njobs, i, x3)) n += job_tasks(i, job_splits(i, c));
+      n += job_tasks(i, job_splits(i, c));
     return n;
   };
   int64_t best_c = std::max(MIN_CHUNK, max_steps), best_cost = -1;
-  static const int forced_rounds = [] {
-    const char* v = getenv("KFAC_SYRK_ROUNDS");
-    return v ? atoi(v) : 0;
-  }();
   // (kfac_factor_tiles_x3: one round -- MNIST MLP with thin-row pairs, same box: 163.4
   // vs 170.3 / 167.4 us per launch at the two rounds the cost model picks)
   const int64_t max_rounds = x3 ? 1 : 4;
-  for (int64_t r = 1; r <= 8; ++r) {
-    if (forced_rounds > 0 ? r != forced_rounds : r > max_rounds) continue;
+  for (int64_t r = 1; r <= 4; ++r) {
+    if (r > max_rounds) continue;
     int64_t lo = MIN_CHUNK, hi = std::max(MIN_CHUNK, max_steps);
     if (tasks_at(hi) > r * slots) continue;  // even one split per tile needs more rounds
     while (lo < hi) {
@@ -2159,11 +2067,6 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
       continue;
     }
     p.splits = (int)job_splits(i, best_c);
-    static const int forced_splits = [] {  // (tuning experiments: KFAC_SYRK_SPLITS)
-      const char* v = getenv("KFAC_SYRK_SPLITS");
-      return v ? atoi(v) : 0;
-    }();
-    if (forced_splits > 0) p.splits = (int)std::min<int64_t>(forced_splits, steps);
     ConvGeom cg;
     if (conv_geom(jobs[i], cg)) {
       // Tasks own whole images, the SAME number k each, and fill the resident slots
@@ -2247,18 +2150,7 @@ struct GroupLaunch {
 
 static int prepare_group(const kfac_factor_job* jobs_in, int njobs, char* ws, size_t ws_bytes,
                          GroupLaunch& g) {
-  // kfac_factor_tiles_x3: the tail jobs (x3_tail) go last, their workgroups dispatched
-  // after the others' (see kfac_factor_tiles_x3) -- a pass's short last batch fills the
-  // slots its full batches' tasks free at the end of the launch
-  const bool x3 = tiles_x3_group(jobs_in, njobs);
-  kfac_factor_job perm[MAXJ];
-  int nmain = 0;
-  for (int pass = 0; pass < 2; ++pass)
-    for (int i = 0; i < njobs; ++i)
-      if (x3_tail(jobs_in, njobs, i, x3) == (pass == 1)) perm[nmain++] = jobs_in[i];
-  nmain = 0;
-  for (int i = 0; i < njobs; ++i) nmain += !x3_tail(jobs_in, njobs, i, x3);
-  const kfac_factor_job* jobs = perm;
+  const kfac_factor_job* jobs = jobs_in;
   Plan plans[MAXJ];
   plan_jobs(jobs, njobs, plans);
   FactorArgs& args = g.args;
@@ -2266,13 +2158,6 @@ static int prepare_group(const kfac_factor_job* jobs_in, int njobs, char* ws, si
   args = FactorArgs{};
   red = FactorArgs{};
   args.njobs = njobs;
-  {
-    static const int stagger = [] {  // (A/B: KFAC_SYRK_STAGGER)
-      const char* e = getenv("KFAC_SYRK_STAGGER");
-      return e ? atoi(e) : 5;
-    }();
-    args.stagger = stagger;
-  }
   {
     const char* e = getenv("KFAC_SYRK_ORDER");
     args.split_major = e ? atoi(e) : 1;
@@ -2308,26 +2193,10 @@ static int prepare_group(const kfac_factor_job* jobs_in, int njobs, char* ws, si
     d.task_begin = tasks;
     tasks += plans[i].tasks;
     args.task_end[i] = tasks;
-    if (i == nmain - 1) args.main_tasks = tasks;
   }
-  if (nmain == njobs || nmain == 0) args.main_tasks = tasks;
   g.tasks = tasks;
   g.rtiles = rtiles;
   g.split_tasks = 0;
-  {
-    static const int inter = [] {
-      const char* e = getenv("KFAC_X3_INTERLEAVE");
-      return e ? atoi(e) : 0;
-    }();
-    bool same = inter && args.split_major;
-    int u = 0;
-    for (int i = 0; i < njobs && same; ++i) {
-      same = plans[i].splits == plans[0].splits && plans[i].tasks == plans[i].units * plans[i].splits;
-      u += plans[i].units;
-      args.unit_end[i] = u;
-    }
-    args.interleave = same;  // (read by kfac_factor_tiles_x3 only)
-  }
   if (syrk3_group(jobs, njobs)) {
     // the pre-split images after the slabs; the split launch's own task ranges
     g.split = args;

@@ -152,11 +152,9 @@ class Curvature(ABC):
 # accumulator starts s0 tiles into it (kfac_factor_job.acc_stride)
 _SLAB_BYTES = 64 * 64 * 4
 
-# A/B: KFAC_SKIP_DONE_WAITS=0 keeps a stream wait on events the host has seen complete
-_SKIP_DONE_WAITS = os.environ.get("KFAC_SKIP_DONE_WAITS", "1") != "0"
-_MERGE_LAUNCHES = os.environ.get("KFAC_MERGE_LAUNCHES", "0") == "1"
-# stream priority of the inversion side streams (-1 high, 0 normal; A/B knob)
-_INV_STREAM_PRIO = int(os.environ.get("KFAC_INV_STREAM_PRIO", "-1"))
+# stream priority of the inversion side streams (-1 high; 0 normal measured within the
+# box spread)
+_INV_STREAM_PRIO = -1
 
 
 def _same_shapes(f, g):
@@ -265,7 +263,7 @@ class KFAC(Curvature):
         self.max_pending = 2
         # one launch for the groups of a queued flush (full batches + short last one);
         # off by default: measured neutral to 2 % slower on the MLP line
-        self.merge_launches = _MERGE_LAUNCHES
+        self.merge_launches = False
         self._inv_streams = {}    # device index -> side streams
 
     def reset(self):
@@ -293,7 +291,7 @@ class KFAC(Curvature):
         ev = self._buf_read.pop(buf.data_ptr(), None)
         if ev is not None:
             # (an event the host already sees complete needs no wait packet on the stream)
-            if not (_SKIP_DONE_WAITS and isinstance(ev, N.RawEvent) and ev.query()):
+            if not (isinstance(ev, N.RawEvent) and ev.query()):
                 self._wait(ev, stream, buf.device)
             self._pool_event(buf.device, ev)  # the wait captured its record: reusable
 
@@ -860,7 +858,7 @@ class KFAC(Curvature):
         if pending.on_side:
             dev = pending.outs[0].device
             if isinstance(pending.done, N.RawEvent):
-                if not (settled and _SKIP_DONE_WAITS):
+                if not settled:
                     pending.done.wait_on(N.stream_handle(dev))
             else:
                 cur = torch.cuda.current_stream(dev)
