@@ -327,6 +327,113 @@ def load_traffic(config):
         return json.load(f).get("hbm_bytes_per_launch")
 
 
+def profiled_steps(N, one_pass, kfac, sync, steps):
+    """`steps` more pipelined steps with the library's HIP-event timing on: {profile
+    slot: (ms, launches)} of the factor-product kernels, the reduce and the inversion."""
+    N.profile_reset()
+    N.profile_enable(True)
+    for _ in range(steps):
+        one_pass()
+    kfac.inv_state
+    sync()
+    N.profile_enable(False)
+    out = {name: N.profile_read(pid) for name, pid in
+           (("kfac_factor_tiles", N.PROF_FACTOR_TILES), ("kfac_factor_syrk3", N.PROF_FACTOR_SYRK3),
+            ("kfac_factor_tiles_x3", N.PROF_FACTOR_X3), ("reduce", N.PROF_FACTOR_REDUCE),
+            ("invert", N.PROF_INVERT))}
+    N.profile_reset()
+    return out
+
+
+def roofline_of(prof, specs, images, steps, config):
+    """The roofline object of the dominant factor-product kernel (the one that took the
+    most time: kfac_factor_tiles / _x3, fp32 or bf16x3 MFMA, or kfac_factor_syrk3) and
+    the per-step kernel breakdown, from profiled_steps' timings of `steps` passes of
+    `images` images: achieved = algorithmic flops / the kernel's launch time."""
+    prods = {k: prof[k] for k in ("kfac_factor_tiles", "kfac_factor_syrk3", "kfac_factor_tiles_x3")}
+    prod_kernel = max(prods, key=lambda k: prods[k][0])
+    tiles_ms, tiles_n = prods[prod_kernel]
+    prods_ms = sum(v[0] for v in prods.values())
+    syrk3 = prod_kernel != "kfac_factor_tiles"
+    fpi = flops_per_image(specs)
+    flops_timed = fpi * images * steps
+    achieved = flops_timed / (tiles_ms * 1e-3) / 1e12 if tiles_ms > 0 else None
+    peak = SYRK3_PEAK_TFLOPS if syrk3 else MFMA_F32_PEAK_TFLOPS
+    roofline = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                "frac": (achieved / peak) if achieved else None,
+                "traffic": load_traffic(config),
+                "kernel": prod_kernel,
+                # (the same rate against the fp32 MFMA peak, the basis of earlier rounds)
+                "frac_fp32_peak_basis": (achieved / MFMA_F32_PEAK_TFLOPS) if achieved else None,
+                "peak_basis": ("dense bf16 MFMA 2.5 PF / 6 products per fp32 product (fp32-equivalent)"
+                               if syrk3 else "dense fp32 MFMA"),
+                "launches": tiles_n,
+                "avg_launch_us": 1e3 * tiles_ms / max(tiles_n, 1),
+                # a launch covers every queued update of the pass (multi-batch jobs):
+                # per-launch figures are the step's algorithmic totals / its launches
+                "flops_per_launch": flops_timed / max(tiles_n, 1),
+                "algorithmic_bytes_per_launch": bytes_per_image(specs) * images * steps
+                                                / max(tiles_n, 1)}
+    breakdown = {"factor_tiles_ms_per_step": prods_ms / steps,
+                 "factor_reduce_ms_per_step": prof["reduce"][0] / steps,
+                 "invert_ms_per_step": prof["invert"][0] / steps}
+    return roofline, breakdown
+
+
+def other_config(config, device, steps, warmup):
+    """A GPU-only line for another BASELINE config on this one GPU (C3 LeNet-5, C5 wide
+    MLP): the same pipelined pass + invert loop as the headline (records resident,
+    eager_verdict False, one launch per records-held cap), `steps` timed steps after
+    `warmup`, then the instrumented repetition for its dominant kernel's roofline."""
+    from bnn_kfac_amd import _native as N
+    from bnn_kfac_amd.curvatures import KFAC
+    specs = CONFIGS[config]
+    batch, images = SHAPES[(config, 1)]
+    net = build_model(config, device)
+    layers = [m for m in net.modules() if isinstance(m, (torch.nn.Linear, torch.nn.Conv2d))]
+    kfac = KFAC(net)
+    kfac.eager_verdict = False
+    kfac.launch_first = 16
+    recs = synthetic_records(specs, images, device, seed=1234)
+    starts = list(range(0, images, batch))
+    views = [[(layer, [a[i:i + batch], g[i:i + batch]]) for layer, (a, g) in zip(layers, recs)]
+             for i in starts]
+    sizes = [min(batch, images - i) for i in starts]
+
+    def one_pass():
+        kfac.reset()
+        for batch_views, size in zip(views, sizes):
+            for layer, rec in batch_views:
+                kfac.record[layer] = rec
+            kfac.update(batch_size=size)
+        kfac.invert(*DAMPING)
+
+    def sync():
+        torch.cuda.synchronize(device)
+
+    for _ in range(warmup):
+        one_pass()
+    kfac.inv_state
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one_pass()
+    kfac.inv_state  # every verdict read inside the timed region
+    sync()
+    elapsed = time.perf_counter() - t0
+    prof = profiled_steps(N, one_pass, kfac, sync, steps)
+    roofline, breakdown = roofline_of(prof, specs, images, steps, config)
+    for h in kfac.hooks:
+        h.remove()
+    del kfac, recs, views
+    torch.cuda.empty_cache()
+    return {"value": images * steps / elapsed, "unit": "images/s", "ms_per_step": 1e3 * elapsed / steps,
+            "steps": steps, "warmup": warmup,
+            "workload": f"{BASELINE_CONFIG[(config, 1)]}: {NAMES[config]} KFAC factor pass over {images} "
+                        f"images (batch {batch}) + invert{DAMPING}, pipelined as the headline",
+            "roofline": roofline, "breakdown": breakdown}
+
+
 # ------------------------------------------------------------------ launcher
 def _free_port():
     with socket.socket() as s:
@@ -397,6 +504,8 @@ def main(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-serial", action="store_true")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="N = 1 MLP: skip the GPU-only C3 (LeNet-5) and C5 (wide MLP) lines")
     ap.add_argument("--launch-first", type=int, default=None,
                     help="queued updates in a pass's first SYRK launch (KFAC.launch_first) for both "
                          "loops (default: 16 for the pipelined loop, the library's 1 for the serial one)")
@@ -568,29 +677,9 @@ def main(argv=None):
     # Kernel durations: the same K steps again with the library's HIP-event timing
     # on (events recorded around each launch, on its stream).  Kept out of the timed
     # region above because the event packets add ~10 us per launch boundary.
-    N.profile_reset()
-    N.profile_enable(True)
     comm["timing"] = True
-    for _ in range(args.steps):
-        one_pass()
-    kfac.inv_state
-    sync()
+    prof = profiled_steps(N, one_pass, kfac, sync, args.steps)
     comm["timing"] = False
-    N.profile_enable(False)
-    # the factor-product kernels: kfac_factor_tiles (fp32 MFMA), kfac_factor_syrk3
-    # (split pass + bf16x3 MFMA, launch groups with a factor of n >= 2048) and
-    # kfac_factor_tiles_x3 (bf16x3 MFMA, fp32 panels split in registers); the roofline
-    # line is the one that took the most time
-    prods = {name: N.profile_read(pid) for name, pid in
-             (("kfac_factor_tiles", N.PROF_FACTOR_TILES), ("kfac_factor_syrk3", N.PROF_FACTOR_SYRK3),
-              ("kfac_factor_tiles_x3", N.PROF_FACTOR_X3))}
-    prod_kernel = max(prods, key=lambda k: prods[k][0])
-    tiles_ms, tiles_n = prods[prod_kernel]
-    prods_ms = sum(v[0] for v in prods.values())
-    syrk3 = prod_kernel != "kfac_factor_tiles"
-    red_ms, red_n = N.profile_read(N.PROF_FACTOR_REDUCE)
-    inv_ms, inv_n = N.profile_read(N.PROF_INVERT)
-    N.profile_reset()
     allreduce_ms = None
     if world > 1:
         allreduce_ms = max_over_ranks(sum(a.elapsed_time(b) for a, b in comm.pop("events", []))
@@ -599,34 +688,10 @@ def main(argv=None):
     images_total = world * images * args.steps
     value = images_total / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
-
-    # roofline of the dominant kernel: algorithmic flops of one launch (= the queued
-    # updates it covers) / its measured duration, averaged over the timed region
-    fpi = flops_per_image(specs)
-    flops_timed = fpi * images * args.steps
-    achieved = flops_timed / (tiles_ms * 1e-3) / 1e12 if tiles_ms > 0 else None
-    peak = SYRK3_PEAK_TFLOPS if syrk3 else MFMA_F32_PEAK_TFLOPS
-    roofline = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                "frac": (achieved / peak) if achieved else None,
-                "traffic": load_traffic(args.config),
-                "kernel": prod_kernel,
-                # (the same rate against the fp32 MFMA peak, the basis of earlier rounds)
-                "frac_fp32_peak_basis": (achieved / MFMA_F32_PEAK_TFLOPS) if achieved else None,
-                "peak_basis": ("dense bf16 MFMA 2.5 PF / 6 products per fp32 product (fp32-equivalent)"
-                               if syrk3 else "dense fp32 MFMA"),
-                "launches": tiles_n,
-                "avg_launch_us": 1e3 * tiles_ms / max(tiles_n, 1),
-                # a launch covers every queued update of the pass (multi-batch jobs):
-                # per-launch figures are the step's algorithmic totals / its launches
-                "flops_per_launch": fpi * images * args.steps / max(tiles_n, 1),
-                "algorithmic_bytes_per_launch": bytes_per_image(specs) * images * args.steps
-                                                / max(tiles_n, 1)}
-    breakdown = {"factor_tiles_ms_per_step": prods_ms / args.steps,
-                 "factor_reduce_ms_per_step": red_ms / args.steps,
-                 "invert_ms_per_step": inv_ms / args.steps,
-                 "allreduce_ms_per_step": allreduce_ms,
-                 "host_issue_ms_per_step": 1e3 * t_issue / args.steps,
-                 "updates_per_step": len(starts)}
+    roofline, breakdown = roofline_of(prof, specs, images, args.steps, args.config)
+    breakdown.update({"allreduce_ms_per_step": allreduce_ms,
+                      "host_issue_ms_per_step": 1e3 * t_issue / args.steps,
+                      "updates_per_step": len(starts)})
 
     serial = None
     if not args.no_serial:
@@ -679,6 +744,16 @@ def main(argv=None):
         sync()
         e2e = images * reps / (time.perf_counter() - t1)
 
+    others = None
+    if world == 1 and args.config == "mlp" and not args.no_other_configs and not args.strong:
+        # BASELINE's other single-GPU configs, GPU-only, in the same run (the records of
+        # the headline pass are freed first)
+        del views, recs
+        record.clear()
+        torch.cuda.empty_cache()
+        others = {"C3": other_config("lenet", device, steps=20, warmup=2),
+                  "C5": other_config("wide", device, steps=10, warmup=2)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the host's best: every thread count this process may use -- its CPU affinity,
@@ -729,7 +804,9 @@ def main(argv=None):
                # N > 1: the sharded pass + all-reduce vs a single-device recompute of the
                # same global batches (verify_parity, after the timed region); N = 1: null
                "parity": None if parity is None else parity["ok"], "parity_detail": parity,
-               "serial_images_per_s": serial, "e2e_images_per_s": e2e}
+               "serial_images_per_s": serial, "e2e_images_per_s": e2e,
+               # BASELINE C3 / C5 on this GPU, same loop (GPU-only; N = 1 MLP runs)
+               "other_configs": others}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -171,7 +171,7 @@ def lib():
 def _release_at_exit():
     try:
         if _lib is not None and torch.cuda.is_initialized():
-            for h in _raw_events:
+            for h in list(_raw_events):
                 _lib.kfac_event_destroy(h)
             _raw_events.clear()
             _lib.kfac_release()
@@ -179,20 +179,38 @@ def _release_at_exit():
         pass
 
 
-_raw_events = []  # handles of every RawEvent made (destroyed at exit, while HIP is up)
+_raw_events = set()  # handles of the live RawEvents (what is left is destroyed at exit)
 
 
 class RawEvent:
     """A HIP event owned through the C ABI (kfac_event_*): record / wait / query /
     synchronize are one ctypes call each, where torch.cuda.Event and Stream objects
-    cost the caller's thread 5-10 us per call.  Kept for the process (pooled)."""
+    cost the caller's thread 5-10 us per call.  Created on `device` (default: the
+    current HIP device), like torch.cuda.Event on its stream's device; destroyed by
+    close() or when the last reference goes (the KFAC event pools hold them)."""
     __slots__ = ("handle",)
 
-    def __init__(self):
+    def __init__(self, device=None):
         h = ctypes.c_void_p()
-        check(lib().kfac_event_create(ctypes.byref(h)), "kfac_event_create")
+        if device is not None and torch.device(device).index is not None:
+            with torch.cuda.device(device):
+                check(lib().kfac_event_create(ctypes.byref(h)), "kfac_event_create")
+        else:
+            check(lib().kfac_event_create(ctypes.byref(h)), "kfac_event_create")
         self.handle = h.value
-        _raw_events.append(self.handle)
+        _raw_events.add(self.handle)
+
+    def close(self):
+        h, self.handle = self.handle, None
+        if h is not None and h in _raw_events:
+            _raw_events.discard(h)
+            _lib.kfac_event_destroy(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # (interpreter shutdown: _release_at_exit owns what is left)
+            pass
 
     def record(self, stream: int):
         check(_lib.kfac_event_record(self.handle, stream), "kfac_event_record")

@@ -2038,9 +2038,12 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
     return n;
   };
   int64_t best_c = std::max(MIN_CHUNK, max_steps), best_cost = -1;
-  // (kfac_factor_tiles_x3: one round -- MNIST MLP with thin-row pairs, same box: 163.4
-  // vs 170.3 / 167.4 us per launch at the two rounds the cost model picks)
-  const int64_t max_rounds = x3 ? 1 : 4;
+  // (kfac_factor_tiles_x3 groups with thin-row pairs: one round -- MNIST MLP, same box:
+  // 163.4 vs 170.3 / 167.4 us per launch at the two rounds the cost model picks; other
+  // x3 groups keep the cost model's choice, which nothing measured against)
+  bool any_thin = false;
+  for (int i = 0; i < njobs && x3; ++i) any_thin |= x3_thin(factor_n(jobs[i]), (int)cdiv(factor_n(jobs[i]), TILE));
+  const int64_t max_rounds = any_thin ? 1 : 4;
   for (int64_t r = 1; r <= 4; ++r) {
     if (r > max_rounds) continue;
     int64_t lo = MIN_CHUNK, hi = std::max(MIN_CHUNK, max_steps);

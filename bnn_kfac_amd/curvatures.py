@@ -791,7 +791,7 @@ class KFAC(Curvature):
         """A raw HIP event (N.RawEvent) from the pool of settled ones (a verdict's `done`
         after its host wait, an ordering event after the wait on it was enqueued)."""
         pool = self._event_pool.get(device.index)
-        return pool.pop() if pool else N.RawEvent()
+        return pool.pop() if pool else N.RawEvent(device)
 
     def _pool_event(self, device, ev):
         self._event_pool.setdefault(device.index, []).append(ev)

@@ -79,6 +79,9 @@ def fake_factor_flush(jobs, device):
 
 def install(monkeypatch):
     from bnn_kfac_amd import _native as N
+    # (accumulators of an earlier test live at host addresses a later test's buffers
+    # may reuse: every test starts with none)
+    ACC.clear()
     monkeypatch.setattr(N, "require_device", lambda t, what, owner=None: None)
     monkeypatch.setattr(N, "factor_update", fake_factor_update)
     monkeypatch.setattr(N, "factor_accum_plan", fake_accum_plan)
@@ -163,8 +166,11 @@ class _NoStream:
 
 class HostRawEvent:
     """Test double of N.RawEvent (host work is synchronous: always complete)."""
-    def __init__(self):
+    def __init__(self, device=None):
         self.handle = 0
+
+    def close(self):
+        pass
 
     def record(self, stream):
         pass

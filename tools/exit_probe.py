@@ -4,6 +4,9 @@ process did before exit:
   factor  -- one kfac_factor_update (ordinary launches), kfac_release at exit
   eig     -- one kfac_syev at n = 4097 (cooperative launch), normal exit
   eig_os  -- the same, then os._exit(0) after flushing (no atexit / static destructors)
+Before it exits the process writes /proc/self/maps to $EXIT_MAPS (if set), so the PCs
+of a crash trace printed during exit can be mapped to a shared object + offset
+(tools/exit_maps.py).
 """
 import json
 import os
@@ -29,7 +32,10 @@ elif mode.startswith("eig"):
     F = X @ X.T / n + 1e-3 * torch.eye(n, device=dev)
     symeig([F])
 torch.cuda.synchronize()
-print(json.dumps({"mode": mode, "done": True}), flush=True)
+print(json.dumps({"mode": mode, "done": True, "pid": os.getpid()}), flush=True)
+if os.environ.get("EXIT_MAPS"):
+    with open("/proc/self/maps") as f, open(os.environ["EXIT_MAPS"], "w") as g:
+        g.write(f.read())
 if mode == "eig_os":
     sys.stdout.flush()
     sys.stderr.flush()
