@@ -30,7 +30,7 @@ c_i32, c_i64, c_f32, c_f64, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_floa
 
 class Operand(ctypes.Structure):
     _fields_ = [("ptr", c_vp), ("layout", c_i32), ("cols", c_i32), ("rows", c_i64),
-                ("has_ones", c_i32), ("reserved0", c_i32), ("ld", c_i64), ("L", c_i64),
+                ("has_ones", c_i32), ("last_rows", c_i32), ("ld", c_i64), ("L", c_i64),
                 ("sB", c_i64)] + [(f, c_i32) for f in
                                   ("C", "H", "W", "kh", "kw", "sh", "sw", "ph", "pw", "Ho", "Wo",
                                    "reserved1")]

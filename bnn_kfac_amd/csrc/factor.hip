@@ -43,6 +43,13 @@ struct FactorJobDev {
   int sstride;       // slabs per tile of `slab` (a job's split s of tile t: t * sstride + s)
   int xsplits;       // x3 thin-row pairs: of the `splits` slabs per tile, the last xsplits are
                      // written by extra, shorter K-splits of the pair units only (x3_xsplits)
+  // ragged last batch (x.last_rows, kfac_factor_tiles_x3 / narrow tasks only): its first
+  // stage `rstage` (-1: none); its rows weigh rows / last_rows = `rw` times the others'
+  // (its own per-batch mean): a task crossing into it scales its sums by 1 / rw = `rinv`
+  // at rstage, and every task ending in it scales by rw at the end
+  int64_t rstage;
+  float rw, rinv;
+  int rdelta;        // rows - last_rows (0: no ragged batch)
 };
 
 struct FactorArgs {
@@ -83,6 +90,22 @@ __device__ __forceinline__ void put_partial(const FactorJobDev& J, const floatx1
 __device__ __forceinline__ const float* seg_base(const FactorJobDev& J, const float* const* segs,
                                                  int seg) {
   return J.seg_off >= 0 ? segs[J.seg_off + seg] : J.x.ptr;
+}
+
+// rows of batch `seg` of a job (its ragged last batch: x.last_rows).  Arithmetic, not a
+// select of two fields: a select of two argument-block addresses makes the compiler
+// copy the whole FactorArgs to scratch (4.5 KB per lane)
+__device__ __forceinline__ int64_t seg_rows(const FactorJobDev& J, int seg) {
+  return J.x.rows - (int64_t)(seg == J.nseg - 1) * J.rdelta;
+}
+
+// the ragged last batch's weight on a task's partial sums (see FactorJobDev::rstage)
+template <int NA>
+__device__ __forceinline__ void scale_acc(floatx16 (&acc)[NA], float f) {
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[a][v] *= f;
 }
 
 struct StageCursor {
@@ -266,12 +289,12 @@ __device__ __forceinline__ void stage_barrier() {
 // column: 1).
 template <int NW = 4>
 __device__ __forceinline__ void narrow_direct_load(const FactorJobDev& J, const float* base, int64_t k0,
-                                                   float (&v)[BK / (2 * NW)]) {
+                                                   int64_t rows, float (&v)[BK / (2 * NW)]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, rr = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int s2 = 0; s2 < BK / (2 * NW); ++s2) {
     const int64_t k = k0 + 2 * (wave * (BK / (2 * NW)) + s2) + h;
-    v[s2] = k < J.x.rows ? (rr < J.x.cols ? base[k * J.x.ld + rr] : (rr == J.x.ones ? 1.f : 0.f)) : 0.f;
+    v[s2] = k < rows ? (rr < J.x.cols ? base[k * J.x.ld + rr] : (rr == J.x.ones ? 1.f : 0.f)) : 0.f;
   }
 }
 
@@ -282,30 +305,32 @@ __device__ __forceinline__ void factor_task_narrow_direct(const FactorJobDev& J,
   const int split = local;  // one tile
   const int64_t s0 = (int64_t)split * J.chunk;
   const int64_t s1 = min(J.nst, s0 + J.chunk);
-  floatx16 acc;
+  floatx16 acc[1];
 #pragma unroll
-  for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+  for (int v = 0; v < 16; ++v) acc[0][v] = 0.f;
   if (s1 > s0) {
     StageCursor c;
     c.init(J, s0);
     const float* base = seg_base(J, segs, c.seg);
     float cur[NV], nxt[NV];
-    narrow_direct_load<NW>(J, base, c.k, cur);
+    narrow_direct_load<NW>(J, base, c.k, seg_rows(J, c.seg), cur);
     for (int64_t s = s0; s < s1; ++s) {
       const int seg = c.seg;
       c.next(J.x.rows);
       if (s + 1 < s1) {
         if (c.seg != seg) base = seg_base(J, segs, c.seg);
-        narrow_direct_load<NW>(J, base, c.k, nxt);
+        narrow_direct_load<NW>(J, base, c.k, seg_rows(J, c.seg), nxt);
       }
+      if (s == J.rstage && s > s0) scale_acc(acc, J.rinv);  // (wave-uniform)
 #pragma unroll
       for (int s2 = 0; s2 < NV; ++s2)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[s2], cur[s2], acc, 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[s2], cur[s2], acc[0], 0, 0, 0);
 #pragma unroll
       for (int s2 = 0; s2 < NV; ++s2) cur[s2] = nxt[s2];
     }
+    if (J.rstage >= 0 && s1 > J.rstage) scale_acc(acc, J.rw);
   }
-  store_narrow<NW>(J, J.slab + (size_t)split * TILE * TILE, acc, lds);
+  store_narrow<NW>(J, J.slab + (size_t)split * TILE * TILE, acc[0], lds);
 }
 
 // NSLOT ring slots (2: one stage in flight, 4 WGs/CU); one barrier per stage.
@@ -888,6 +913,8 @@ __device__ __forceinline__ void x3_loop(const FactorJobDev& J, const float* cons
   const int ld4 = (int)J.x.ld * 4;
   const int rows = (int)J.x.rows;
   const int rec = rows * ld4;                  // a batch's bytes (planner: < 2^31)
+  // (the ragged last batch's: its rows past x.last_rows read as zeros)
+  const int rec_last = rec - J.rdelta * ld4;
   const int lr = 16 * wave + 8 * (lane >> 5);  // lane's first row within a stage
   int voff[4];
   bool onesl[4];
@@ -916,38 +943,40 @@ __device__ __forceinline__ void x3_loop(const FactorJobDev& J, const float* cons
     nb = seg_base(J, segs, min(c.seg + 1, lastseg));
     left -= more;
   };
-  auto rsrc = [&](const float* b) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(b), 0, rec, 0x00020000);
+  auto rsrc = [&](const float* b, int seg) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(b), 0, seg == lastseg ? rec_last : rec,
+                                             0x00020000);
   };
   auto ld8 = [&](int f, const X3Cursor& c, float (&x)[8]) {
-    x3_load8(x, rsrc(c.b), X3Col{voff[f], false, 0.f}, c.k * ld4, ld4);
+    x3_load8(x, rsrc(c.b, c.seg), X3Col{voff[f], false, 0.f}, c.k * ld4, ld4);
   };
   float x[4][8];
   // prologue: stage s0 into every fragment, the first block's fragments split, their
   // registers reloaded with stage s0 + 1
-  const int k0 = c2.k;
+  const int k0 = c2.k, seg0 = c2.seg;
 #pragma unroll
   for (int f = 0; f < 4; ++f)
     if (USE[f]) ld8(f, c2, x[f]);
   advance(c2);
   X3Cursor c1 = c2;  // (fragments 1 / 3 load stage s0 + 1 in the first stage)
-  int kc = k0;       // first row of the stage being multiplied
-  auto fix = [&](int f, int kstage) {  // the ones column: 1 on the batch's rows, 0 past them
+  int kc = k0, kcs = seg0;  // first row and batch of the stage being multiplied
+  auto fix = [&](int f, int kstage, int kseg) {  // the ones column: 1 on the batch's rows, 0 past them
     if constexpr (FILL) {
-      const int nvalid = rows - kstage;
+      const int nvalid = (int)seg_rows(J, kseg) - kstage;
 #pragma unroll
       for (int r = 0; r < 8; ++r) x[f][r] = onesl[f] ? (lr + r < nvalid ? 1.f : 0.f) : x[f][r];
     }
   };
-  // split fragment f (of the stage starting at row kstage) and reload its registers
-  auto take = [&](int f, int kstage, const X3Cursor& c) {
-    fix(f, kstage);
+  // split fragment f (of the stage starting at row kstage of batch kseg) and reload its
+  // registers
+  auto take = [&](int f, int kstage, int kseg, const X3Cursor& c) {
+    fix(f, kstage, kseg);
     const X3Frag fr = x3_split8(x[f]);
     ld8(f, c, x[f]);
     return fr;
   };
-  X3Frag pa = take(0, k0, c2);
-  X3Frag pb = SAME ? pa : take(2, k0, c2);
+  X3Frag pa = take(0, k0, seg0, c2);
+  X3Frag pb = SAME ? pa : take(2, k0, seg0, c2);
   // the prologue's loads complete here (once per task): the loop header then starts
   // from a precise wait state, and the compiler keeps the counted vmcnt at the top of
   // each stage (with the prologue's loads still in flight it merged them into a
@@ -957,21 +986,21 @@ __device__ __forceinline__ void x3_loop(const FactorJobDev& J, const float* cons
   constexpr int NV = FILL ? 52 / 6 + 1 : 44 / 6 + 1;
   // one stage: P = (A0, B0) of this stage in, (A0', B0') of the next stage out
   auto stage = [&](const X3Frag& A0, const X3Frag& B0, X3Frag& A0n, X3Frag& B0n) {
-    const int kn = c2.k;  // first row of the next stage (in x0 / x2 now)
+    const int kn = c2.k, kns = c2.seg;  // first row / batch of the next stage (in x0 / x2 now)
     // the cursors: x1 / x3 reload the next stage, x0 / x2 the one after
     c1 = c2;
     advance(c2);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (PAIR) {  // B0 = C0
-      const X3Frag A1 = take(1, kc, c1);
+      const X3Frag A1 = take(1, kc, kcs, c1);
       x3_six(acc[0][0], A0, A0);
       x3_pattern<NV>();
       __builtin_amdgcn_sched_barrier(0);
-      A0n = take(0, kn, c2);
+      A0n = take(0, kn, kns, c2);
       x3_six(acc[0][1], B0, A0);
       x3_pattern<NV>();
       __builtin_amdgcn_sched_barrier(0);
-      B0n = take(2, kn, c2);
+      B0n = take(2, kn, kns, c2);
       x3_six(acc[1][0], A1, A0);
       x3_pattern<NV>();
       __builtin_amdgcn_sched_barrier(0);
@@ -981,64 +1010,87 @@ __device__ __forceinline__ void x3_loop(const FactorJobDev& J, const float* cons
       x3_six(acc4, B0, A1);
       x3_pattern<0>();
     } else if constexpr (MASK == 15) {
-      const X3Frag A1 = take(1, kc, c1);
+      const X3Frag A1 = take(1, kc, kcs, c1);
       x3_six(acc[0][0], A0, B0);
       x3_pattern<NV>();
       __builtin_amdgcn_sched_barrier(0);
-      const X3Frag B1 = take(3, kc, c1);
+      const X3Frag B1 = take(3, kc, kcs, c1);
       x3_six(acc[1][0], A1, B0);
       x3_pattern<NV>();
       __builtin_amdgcn_sched_barrier(0);
-      A0n = take(0, kn, c2);
+      A0n = take(0, kn, kns, c2);
       x3_six(acc[0][1], A0, B1);
       x3_pattern<NV>();
       __builtin_amdgcn_sched_barrier(0);
-      B0n = take(2, kn, c2);
+      B0n = take(2, kn, kns, c2);
       x3_six(acc[1][1], A1, B1);
       x3_pattern<NV>();
     } else if constexpr (MASK == 13) {  // diagonal: (0,0) (1,0) (1,1), B = A
-      const X3Frag A1 = take(1, kc, c1);
+      const X3Frag A1 = take(1, kc, kcs, c1);
       x3_six(acc[0][0], A0, A0);
       x3_pattern<NV>();
       __builtin_amdgcn_sched_barrier(0);
       x3_six(acc[1][0], A1, A0);
-      A0n = take(0, kn, c2);
+      A0n = take(0, kn, kns, c2);
       x3_pattern<NV>();
       __builtin_amdgcn_sched_barrier(0);
       x3_six(acc[1][1], A1, A1);
       x3_pattern<0>();
       B0n = A0n;
     } else if constexpr (MASK == 5) {  // (0,0) (1,0)
-      const X3Frag A1 = take(1, kc, c1);
+      const X3Frag A1 = take(1, kc, kcs, c1);
       x3_six(acc[0][0], A0, B0);
       x3_pattern<NV>();
       __builtin_amdgcn_sched_barrier(0);
-      A0n = take(0, kn, c2);
-      B0n = take(2, kn, c2);
+      A0n = take(0, kn, kns, c2);
+      B0n = take(2, kn, kns, c2);
       x3_six(acc[1][0], A1, B0);
       x3_pattern<2 * NV>();
     } else if constexpr (MASK == 3) {  // (0,0) (0,1): the last tile row of a factor
-      const X3Frag B1 = take(3, kc, c1);
+      const X3Frag B1 = take(3, kc, kcs, c1);
       x3_six(acc[0][0], A0, B0);
       x3_pattern<NV>();
       __builtin_amdgcn_sched_barrier(0);
-      A0n = take(0, kn, c2);
-      B0n = take(2, kn, c2);
+      A0n = take(0, kn, kns, c2);
+      B0n = take(2, kn, kns, c2);
       x3_six(acc[0][1], A0, B1);
       x3_pattern<2 * NV>();
     } else {  // 1: the last diagonal tile, (0,0) only, B = A
-      A0n = take(0, kn, c2);
+      A0n = take(0, kn, kns, c2);
       x3_six(acc[0][0], A0, A0);
       x3_pattern<NV>();
       B0n = A0n;
     }
     kc = kn;
+    kcs = kns;
   };
+  // the ragged last batch: sums so far scaled by 1 / rw where the task crosses into it,
+  // everything by rw at the end when it reaches it (FactorJobDev::rstage)
+  const int64_t rst = J.rstage;
+  const int bst = (rst > s0 && rst < s1) ? (int)(rst - s0) : -1;
   for (int st = 0; st < ns; ++st) {
+    if (st == bst) {
+      scale_acc(acc[0], J.rinv);
+      scale_acc(acc[1], J.rinv);
+      if constexpr (PAIR) {
+        floatx16 a4[1] = {acc4};
+        scale_acc(a4, J.rinv);
+        acc4 = a4[0];
+      }
+    }
     X3Frag qa, qb;
     stage(pa, pb, qa, qb);
     pa = qa;
     pb = qb;
+  }
+  if (rst >= 0 && s1 > rst) {
+    scale_acc(acc[0], J.rw);
+    scale_acc(acc[1], J.rw);
+    if constexpr (PAIR) {
+      floatx16 a4[1] = {acc4};
+      scale_acc(a4, J.rw);
+      acc4 = a4[0];
+    }
   }
 }
 
@@ -1494,7 +1546,7 @@ __global__ __launch_bounds__(NTHREADS, (CB == 2 && !M3) ? KFAC_CONV_OCC : 4) voi
                 [&](float a, float b) { acc16 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc16, 0, 0, 0); });
       return;
     }
-    if (CB == 2 && nmine == 2) {
+    if constexpr (CB == 2) if (nmine == 2) {
       // both blocks in one pass, their MFMAs alternating (two independent chains)
       row_mfmas2(cimg + (zeroA ? cg.zero_base : offA[0] + rowA), cimg + offB[0] + rowB,
                  cimg + (zeroA ? cg.zero_base : offA[1] + rowA), cimg + offB[1] + rowB);
@@ -1902,7 +1954,14 @@ static int factor_n(const kfac_factor_job& j) { return j.x.cols + (j.x.has_ones 
 // K stages (BK rows each, never straddling two batches) of a job.
 static int64_t job_sps(const kfac_factor_job& j) { return std::max<int64_t>(1, cdiv(j.x.rows, BK)); }
 static int job_nseg(const kfac_factor_job& j) { return j.nseg > 1 ? j.nseg : 1; }
-static int64_t job_stages(const kfac_factor_job& j) { return job_sps(j) * job_nseg(j); }
+// a multi-batch job whose last batch is shorter (x.last_rows)
+static bool job_ragged(const kfac_factor_job& j) {
+  return j.nseg > 1 && j.x.last_rows > 0 && j.x.last_rows < j.x.rows;
+}
+static int64_t job_stages(const kfac_factor_job& j) {
+  if (job_ragged(j)) return job_sps(j) * (j.nseg - 1) + std::max<int64_t>(1, cdiv(j.x.last_rows, BK));
+  return job_sps(j) * job_nseg(j);
+}
 
 // Split K so that the grouped launch fills the chip's workgroup slots (256 CUs x 4
 // resident workgroups) in as few dispatch rounds as possible with every task still
@@ -1945,7 +2004,7 @@ static size_t split3_bytes(const kfac_factor_job& j) {
   const int n = factor_n(j);
   if (n <= 32) return 0;
   const int64_t t3 = cdiv(n, MT);
-  return align_up((size_t)(job_sps(j) * job_nseg(j)) * (size_t)t3 * S3_PANEL, 256);
+  return align_up((size_t)job_stages(j) * (size_t)t3 * S3_PANEL, 256);
 }
 
 static bool syrk3_group(const kfac_factor_job* jobs, int njobs) {
@@ -2133,6 +2192,15 @@ static void fill_dev(FactorJobDev& d, const kfac_factor_job& jb) {
   d.nseg = job_nseg(jb);
   d.sps = (int)job_sps(jb);
   d.nst = job_stages(jb);
+  d.rstage = -1;
+  d.rw = d.rinv = 1.f;
+  d.rdelta = 0;
+  if (job_ragged(jb)) {
+    d.rdelta = (int)(jb.x.rows - jb.x.last_rows);
+    d.rstage = (int64_t)d.sps * (jb.nseg - 1);
+    d.rw = (float)((double)jb.x.rows / (double)jb.x.last_rows);
+    d.rinv = (float)((double)jb.x.last_rows / (double)jb.x.rows);
+  }
 }
 
 // One reduce launch over `njobs` jobs whose slabs are described by d.slab/d.splits.
@@ -2340,6 +2408,9 @@ static int validate(const kfac_factor_job* jobs, int njobs) {
       return KFAC_EINVAL;
     if (j.nseg < 0 || (j.nseg > 1 && !j.seg_ptrs) || job_sps(j) > (1 << 30))
       return KFAC_EINVAL;
+    if (j.x.last_rows < 0 || j.x.last_rows > j.x.rows ||
+        (job_ragged(j) && j.x.layout != KFAC_ROWMAJOR))
+      return KFAC_EINVAL;
   }
   return KFAC_OK;
 }
@@ -2364,6 +2435,106 @@ extern "C" int kfac_factor_accum_plan(const kfac_factor_job* jobs, int njobs, in
   return KFAC_OK;
 }
 
+// One launch group of kfac_factor_update.  A ragged multi-batch job (x.last_rows) runs
+// in one launch on kfac_factor_tiles_x3 (and its narrow tasks); any other kernel, or a
+// group past the launch's KSEG batch bases, takes it as two launches: the equal batches,
+// then the last batch as a job of its own (alpha * rows / last_rows, adding).
+static int update_group(const kfac_factor_job* gj, int n, void* workspace, size_t workspace_bytes,
+                        kfac_stream_t stream) {
+  bool ragged = false;
+  int nbases = 0;
+  for (int k = 0; k < n; ++k) {
+    ragged |= job_ragged(gj[k]);
+    nbases += job_nseg(gj[k]) > 1 ? gj[k].nseg : 0;
+  }
+  if (ragged && (!tiles_x3_group(gj, n) || nbases > KSEG)) {
+    std::vector<kfac_factor_job> head(gj, gj + n), tail;
+    for (kfac_factor_job& j : head) {
+      if (!job_ragged(j)) continue;
+      const float* const* bases = reinterpret_cast<const float* const*>(j.seg_ptrs);
+      kfac_factor_job t = j;
+      t.x.ptr = bases[j.nseg - 1];
+      t.x.rows = j.x.last_rows;
+      t.x.last_rows = 0;
+      t.seg_ptrs = nullptr;
+      t.nseg = 0;
+      t.alpha = (float)((double)j.alpha * (double)j.x.rows / (double)j.x.last_rows);
+      if (t.acc) t.acc_beta = 1.f;
+      else t.beta = 1.f;
+      tail.push_back(t);
+      j.x.last_rows = 0;
+      if (--j.nseg == 1) {
+        j.x.ptr = bases[0];
+        j.seg_ptrs = nullptr;
+        j.nseg = 0;
+      }
+    }
+    int rc = update_group(head.data(), n, workspace, workspace_bytes, stream);
+    if (rc != KFAC_OK) return rc;
+    return update_group(tail.data(), (int)tail.size(), workspace, workspace_bytes, stream);
+  }
+  ConvGeom cg;
+  if (n == 1 && gj[0].x.layout != KFAC_ROWMAJOR && job_nseg(gj[0]) > 1 && !conv_geom(gj[0], cg)) {
+    // a multi-batch conv job off the image-staged kernel (images too large for LDS):
+    // the register-staged kernels read one batch base, so one launch per batch,
+    // each adding to what the previous one wrote
+    const float* const* bases = reinterpret_cast<const float* const*>(gj[0].seg_ptrs);
+    for (int s = 0; s < gj[0].nseg; ++s) {
+      kfac_factor_job j = gj[0];
+      j.seg_ptrs = nullptr;
+      j.nseg = 0;
+      j.x.ptr = bases[s];
+      if (s > 0) {
+        if (j.acc) j.acc_beta = 1.f;
+        else j.beta = 1.f;
+      }
+      const int rc = factor_group(&j, 1, (char*)workspace, workspace_bytes, (hipStream_t)stream);
+      if (rc != KFAC_OK) return rc;
+    }
+    return KFAC_OK;
+  }
+  int multi = 0, maxseg = 1, total = 0;
+  for (int k = 0; k < n; ++k)
+    if (job_nseg(gj[k]) > 1) {
+      ++multi;
+      maxseg = std::max(maxseg, gj[k].nseg);
+      total += gj[k].nseg;
+    }
+  if (total <= KSEG) {
+    const int rc = factor_group(gj, n, (char*)workspace, workspace_bytes, (hipStream_t)stream);
+    if (rc != KFAC_OK) return rc;
+    return KFAC_OK;
+  }
+  // more batch bases than one launch's kernel arguments hold: rounds of S batches
+  // per multi-batch job, each round adding to what the previous ones wrote
+  const int S = KSEG / multi;  // >= KSEG / MAXJ = 4
+  for (int r = 0; r * S < maxseg; ++r) {
+    std::vector<kfac_factor_job> sub;
+    for (int k = 0; k < n; ++k) {
+      kfac_factor_job j = gj[k];
+      if (job_nseg(j) > 1) {
+        const int b0 = r * S;
+        if (b0 >= j.nseg) continue;
+        const float* const* bases = reinterpret_cast<const float* const*>(j.seg_ptrs) + b0;
+        j.seg_ptrs = bases;
+        j.nseg = std::min(S, j.nseg - b0);
+        j.x.ptr = bases[0];
+      } else if (r > 0) {
+        continue;
+      }
+      if (r > 0) {
+        if (j.acc) j.acc_beta = 1.f;
+        else j.beta = 1.f;
+      }
+      sub.push_back(j);
+    }
+    const int rc = factor_group(sub.data(), (int)sub.size(), (char*)workspace, workspace_bytes,
+                                (hipStream_t)stream);
+    if (rc != KFAC_OK) return rc;
+  }
+  return KFAC_OK;
+}
+
 extern "C" int kfac_factor_update(const kfac_factor_job* jobs, int njobs, void* workspace,
                                   size_t workspace_bytes, kfac_stream_t stream) {
   const int rc0 = validate(jobs, njobs);
@@ -2374,66 +2545,8 @@ extern "C" int kfac_factor_update(const kfac_factor_job* jobs, int njobs, void* 
   std::vector<std::pair<int, int>> groups;
   launch_groups(jobs, njobs, sorted, order, groups);
   for (const auto& g : groups) {
-    const kfac_factor_job* gj = sorted.data() + g.first;
-    ConvGeom cg;
-    if (g.second == 1 && gj[0].x.layout != KFAC_ROWMAJOR && job_nseg(gj[0]) > 1 && !conv_geom(gj[0], cg)) {
-      // a multi-batch conv job off the image-staged kernel (images too large for LDS):
-      // the register-staged kernels read one batch base, so one launch per batch,
-      // each adding to what the previous one wrote
-      const float* const* bases = reinterpret_cast<const float* const*>(gj[0].seg_ptrs);
-      for (int s = 0; s < gj[0].nseg; ++s) {
-        kfac_factor_job j = gj[0];
-        j.seg_ptrs = nullptr;
-        j.nseg = 0;
-        j.x.ptr = bases[s];
-        if (s > 0) {
-          if (j.acc) j.acc_beta = 1.f;
-          else j.beta = 1.f;
-        }
-        const int rc = factor_group(&j, 1, (char*)workspace, workspace_bytes, (hipStream_t)stream);
-        if (rc != KFAC_OK) return rc;
-      }
-      continue;
-    }
-    int multi = 0, maxseg = 1, total = 0;
-    for (int k = 0; k < g.second; ++k)
-      if (job_nseg(gj[k]) > 1) {
-        ++multi;
-        maxseg = std::max(maxseg, gj[k].nseg);
-        total += gj[k].nseg;
-      }
-    if (total <= KSEG) {
-      const int rc = factor_group(gj, g.second, (char*)workspace, workspace_bytes, (hipStream_t)stream);
-      if (rc != KFAC_OK) return rc;
-      continue;
-    }
-    // more batch bases than one launch's kernel arguments hold: rounds of S batches
-    // per multi-batch job, each round adding to what the previous ones wrote
-    const int S = KSEG / multi;  // >= KSEG / MAXJ = 4
-    for (int r = 0; r * S < maxseg; ++r) {
-      std::vector<kfac_factor_job> sub;
-      for (int k = 0; k < g.second; ++k) {
-        kfac_factor_job j = gj[k];
-        if (job_nseg(j) > 1) {
-          const int b0 = r * S;
-          if (b0 >= j.nseg) continue;
-          const float* const* bases = reinterpret_cast<const float* const*>(j.seg_ptrs) + b0;
-          j.seg_ptrs = bases;
-          j.nseg = std::min(S, j.nseg - b0);
-          j.x.ptr = bases[0];
-        } else if (r > 0) {
-          continue;
-        }
-        if (r > 0) {
-          if (j.acc) j.acc_beta = 1.f;
-          else j.beta = 1.f;
-        }
-        sub.push_back(j);
-      }
-      const int rc = factor_group(sub.data(), (int)sub.size(), (char*)workspace, workspace_bytes,
-                                  (hipStream_t)stream);
-      if (rc != KFAC_OK) return rc;
-    }
+    const int rc = update_group(sorted.data() + g.first, g.second, workspace, workspace_bytes, stream);
+    if (rc != KFAC_OK) return rc;
   }
   return KFAC_OK;
 }

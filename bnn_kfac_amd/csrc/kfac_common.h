@@ -43,6 +43,7 @@ struct ProfScope {
 struct OpDev {
   const float* ptr;
   int64_t rows;
+  int64_t last_rows;  // multi-batch ROWMAJOR job: rows of the ragged last batch (0: rows)
   int64_t ld, L, sB;
   int32_t layout, cols, ones;  // ones = cols if has_ones else -1
   int32_t C, H, W, kh, kw, sh, sw, ph, pw, Ho, Wo;
@@ -52,6 +53,7 @@ static inline OpDev to_dev(const kfac_operand& o) {
   OpDev d;
   d.ptr = o.ptr;
   d.rows = o.rows;
+  d.last_rows = o.last_rows;
   d.ld = o.ld;
   d.L = o.L;
   d.sB = o.sB;

@@ -157,6 +157,23 @@ _SLAB_BYTES = 64 * 64 * 4
 _INV_STREAM_PRIO = -1
 
 
+# The inversion side streams, one pair per device for the whole process: a KFAC object
+# made after another (a new model, a new epoch's object) takes the same HIP streams.  New
+# streams per object measured the second object's LeNet-5 line at 1.03e7 instead of
+# 1.53e7 img/s (tools/other_probe.py twice): with more streams than the device's hardware
+# queues (GPU_MAX_HW_QUEUES), a new side stream can share its queue with the caller's
+# stream, and the inversion then no longer runs beside the next pass.
+_SIDE_STREAMS = {}
+
+
+def _shared_side_streams(device):
+    pair = _SIDE_STREAMS.get(device.index)
+    if pair is None:
+        pair = _SIDE_STREAMS[device.index] = [torch.cuda.Stream(device=device, priority=_INV_STREAM_PRIO)
+                                              for _ in range(2)]
+    return pair
+
+
 def _same_shapes(f, g):
     """Two fast-path templates of the same record signature (layers, shapes, strides)."""
     return all(a[:7] == b[:7] for a, b in zip(f[1], g[1])) and len(f[1]) == len(g[1])
@@ -625,9 +642,20 @@ class KFAC(Curvature):
             if i == len(queue) or queue[i][5] is not queue[start][5] or align[i] != align[start]:
                 groups.append(queue[start:i])
                 start = i
+        align = {id(e): a for e, a in zip(queue, align)}
+        # a pass's short last batch joins the batches before it as the ragged last
+        # batch of their multi-batch jobs (x.last_rows): one launch instead of two
+        ragged = [False] * len(groups)
+        i = 0
+        while i + 1 < len(groups):
+            if len(groups[i + 1]) == 1 and self._ragged_ok(groups[i], groups[i + 1][0], align):
+                groups[i] = groups[i] + groups[i + 1]
+                del groups[i + 1]
+                ragged[i] = True
+            i += 1
         tables = []
         launches = []
-        for group in groups:
+        for group, rag in zip(groups, ragged):
             tmpl = group[0][0]
             jobs = []
             for k, t in enumerate(tmpl):
@@ -637,6 +665,8 @@ class KFAC(Curvature):
                     table = N.segment_table([e[1][k] for e in group])
                     tables.append(table)
                     job.seg_ptrs, job.nseg = N.table_ptr(table), len(group)
+                    if rag:
+                        job.x.last_rows = group[-1][0][k].x.rows
                     jobs.append(job)
                 else:
                     for i, e in enumerate(group):
@@ -660,6 +690,28 @@ class KFAC(Curvature):
         # calls); the caching allocator orders any reuse of the records' memory after
         # the launches on this stream
         del tables, queue
+
+    @staticmethod
+    def _ragged_ok(group, last, align):
+        """`last` (one queued update) can be the ragged last batch of `group`'s
+        multi-batch jobs: the same row-major factors, fewer rows, the per-batch-mean
+        weighting (alpha x rows equal: the library weighs the last batch by
+        rows / last_rows), the same operand alignment."""
+        if align is not None and align[id(group[0])] != align[id(last)]:
+            return False
+        ta, tb = group[0][0], last[0]
+        if len(ta) != len(tb):
+            return False
+        for a, b in zip(ta, tb):
+            xa, xb = a.x, b.x
+            if (xa.layout != N.ROWMAJOR or xb.layout != N.ROWMAJOR or xa.cols != xb.cols
+                    or xa.has_ones != xb.has_ones or xa.ld != xb.ld or a.F != b.F
+                    or xa.last_rows or xb.last_rows or not 0 < xb.rows < xa.rows):
+                return False
+            wa, wb = a.alpha * xa.rows, b.alpha * xb.rows
+            if not abs(wa - wb) <= 1e-6 * abs(wa):
+                return False
+        return True
 
     def _acc_takes(self, jobs, device):
         """A launch of `jobs` fits the pending accumulation cycle: every factor it
@@ -839,8 +891,7 @@ class KFAC(Curvature):
         chip (wide MLP: 13.8 -> 25.5 ms per inversion when they did)."""
         s = self._inv_streams.get(device.index)
         if s is None:
-            s = self._inv_streams[device.index] = [torch.cuda.Stream(device=device, priority=_INV_STREAM_PRIO)
-                                                   for _ in range(2)]
+            s = self._inv_streams[device.index] = _shared_side_streams(device)
         if not isinstance(s, list):  # a single stream set by hand (tools/probe_*.py)
             return s
         if not alternate:

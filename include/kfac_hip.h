@@ -58,7 +58,12 @@ typedef struct kfac_operand {
   int32_t cols;
   int64_t rows;
   int32_t has_ones;
-  int32_t reserved0;
+  /* Multi-batch ROWMAJOR job (nseg > 1): rows of its LAST batch when that batch is
+   * shorter than `rows` (a pass's ragged last batch), 0 = every batch has `rows`.
+   * That batch enters with its own per-batch mean, alpha * rows / last_rows (the
+   * reference's `/ forward.shape[1]` per update, curvatures.py:349,356); the other
+   * batches with alpha.                                                       */
+  int32_t last_rows;
   int64_t ld;  /* ROWMAJOR row stride (elements) */
   int64_t L;   /* CHANNEL/PATCH: positions per sample (Ho*Wo) */
   int64_t sB;  /* CHANNEL/PATCH: sample stride (elements) */

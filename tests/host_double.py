@@ -29,10 +29,18 @@ def fake_factor_update(jobs, device):
             bases = np.ctypeslib.as_array((ctypes.c_int64 * j.nseg).from_address(j.seg_ptrs))
         else:
             bases = [op.ptr]
-        X = np.concatenate([_view(int(b), op.rows * op.ld).reshape(op.rows, op.ld)[:, :op.cols]
-                            for b in bases]).astype(np.float64)
+        # a ragged last batch (x.last_rows) enters with weight rows / last_rows
+        rows = [op.rows] * len(bases)
+        if j.nseg > 1 and 0 < op.last_rows < op.rows:
+            rows[-1] = op.last_rows
+        Xs = []
+        for b, r in zip(bases, rows):
+            Xb = _view(int(b), r * op.ld).reshape(r, op.ld)[:, :op.cols].astype(np.float64)
+            Xs.append(Xb * np.sqrt(op.rows / r))
+        X = np.concatenate(Xs)
         if op.has_ones:
-            X = np.concatenate([X, np.ones((X.shape[0], 1))], axis=1)
+            ones = np.concatenate([np.full((r, 1), np.sqrt(op.rows / r)) for r in rows])
+            X = np.concatenate([X, ones], axis=1)
         n = op.cols + op.has_ones
         if j.acc:
             # (modelled per slab range: ACC[acc pointer] = that range's n x n partial sum)

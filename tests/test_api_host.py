@@ -201,15 +201,16 @@ def test_queued_updates_merge_into_multibatch_jobs(monkeypatch):
     for g, w in zip(got, want):
         np.testing.assert_allclose(g, w, rtol=1e-6)
     # a first launch of 16 queued updates: the whole pass is queued until the flush,
-    # one multi-batch job per merge group, all groups in ONE launch (each factor's
-    # three jobs on their own accumulator slab ranges): [8 8 8 | 5 | 8 8]
+    # one multi-batch job per merge group, the short batch the ragged last batch of the
+    # group before it (x.last_rows), all groups in ONE launch (each factor's two jobs on
+    # their own accumulator slab ranges): [8 8 8 5* | 8 8]
     got, launches = run(True, launch_first=16)
-    assert launches == [[3] * 4 + [1] * 4 + [2] * 4]
+    assert launches == [[4] * 4 + [2] * 4]
     for g, w in zip(got, want):
         np.testing.assert_allclose(g, w, rtol=1e-6)
     # merge_launches off: one launch call per merge group
     got, launches = run(True, launch_first=16, merge=False)
-    assert launches == [[3] * 4, [1] * 4, [2] * 4]
+    assert launches == [[4] * 4, [2] * 4]
     for g, w in zip(got, want):
         np.testing.assert_allclose(g, w, rtol=1e-6)
     # defer_bytes caps the records a queue holds: an 8-row update keeps 608 bytes,

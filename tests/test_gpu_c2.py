@@ -1,11 +1,11 @@
 """GPU parity at BASELINE C2's stated config, run exactly as bench.py's headline loop
 runs it: the MLP 784-128-10 over one MNIST-sized pass of 60,000 images at batch
 4,096 (14 full batches + a 2,656-row last batch), KFAC.launch_first 16 (the pass's
-queued updates go out at the flush: one multi-batch x3 launch for the full batches
-with the planner's K-split plan -- f full-tile K-splits plus the thin-row pair units'
-extra K-splits -- and one for the short batch), deferred reduction, double-buffered
-state, eager_verdict False and invert(0.04, 200) pipelined: pass 2 is queued behind
-inversion 1 on its side stream before any verdict is read.
+queued updates go out at the flush as ONE multi-batch x3 launch: the full batches and
+the short last batch as its ragged last segment, with the planner's K-split plan -- f
+full-tile K-splits plus the thin-row pair units' extra K-splits), deferred reduction,
+double-buffered state, eager_verdict False and invert(0.04, 200) pipelined: pass 2 is
+queued behind inversion 1 on its side stream before any verdict is read.
 
 Every A / G of pass 2 against the fp64 oracle (models/curvatures.py:345-363:
 O.linear_factor_A / O.grad_factor, sum of per-batch means) at rtol 1e-5, and every L
@@ -41,7 +41,8 @@ def test_mlp_c2_bench_pass_pipelined_vs_fp64_oracle(hip_device):
     orig = N.factor_update
 
     def counting(jobs, device):
-        launches.append([j.x.rows * max(j.nseg, 1) for j in jobs])
+        launches.append([(j.x.rows * (j.nseg - 1) + (j.x.last_rows or j.x.rows)) if j.nseg > 1
+                         else j.x.rows for j in jobs])
         return orig(jobs, device)
 
     def one_pass():
@@ -62,11 +63,9 @@ def test_mlp_c2_bench_pass_pipelined_vs_fp64_oracle(hip_device):
         inv = kfac.inv_state  # settles both verdicts
     finally:
         N.factor_update = orig
-    # the headline's launch structure: per pass one launch of the 14 full batches'
-    # multi-batch jobs and one of the short batch's
-    assert len(launches) == 4, launches
-    assert all(rows == [14 * BATCH] * 4 for rows in launches[0::2]), launches
-    assert all(rows == [2656] * 4 for rows in launches[1::2]), launches
+    # the headline's launch structure: ONE launch per pass, every factor one multi-batch
+    # job over the 14 full batches and the 2,656-row last one (x.last_rows)
+    assert launches == [[IMAGES] * 4] * 2, launches
     state = [[t.cpu().numpy() for t in kfac.state[m]] for m in layers]
     Ls = [[t.cpu().numpy() for t in inv[m]] for m in layers]
     for a, b in zip(L1, [t for m in layers for t in inv[m]]):
