@@ -8,7 +8,7 @@ TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-BENCH=${BENCH:-"python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e --no-serial"}  # (the pipelined loop only: its launches are the roofline line's) override for other configs
+BENCH=${BENCH:-"python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e --no-serial --no-other-configs"}  # (the pipelined loop only: its launches are the roofline line's) override for other configs
 ok() { [ "$1" -le 2 ]; }   # 0 ok, 1/2 = profiler/usage error (no GPU fault)
 
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $BENCH > $OUT/trace.log 2>&1

@@ -11,3 +11,7 @@ python -c "
 import json;d=json.loads(open('$O/bench_mlp.log').read().strip().splitlines()[-1])
 print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline']['avg_launch_us'], d['serial_images_per_s'], d['breakdown'])
 for k,v in d['other_configs'].items(): print(k, v['value'], v['ms_per_step'], v['roofline']['kernel'], v['roofline']['frac'], v['breakdown'])"
+timeout -k 10 150 python tools/step_timeline.py 60 > $O/timeline.log 2>&1 || { tail -20 $O/timeline.log; exit 1; }
+tail -1 $O/timeline.log
+bash profiles/collect.sh r05pmc > $O/collect.log 2>&1 || { tail -20 $O/collect.log; exit 1; }
+tail -8 $O/collect.log
