@@ -315,9 +315,11 @@ def factor_accum_plan(jobs):
     return list(zip(splits, nbytes))
 
 
-def factor_flush(jobs, device: torch.device):
+def factor_flush(jobs, device: torch.device, stream: int = None):
+    """kfac_factor_flush on torch's current stream, or on the raw HIP stream `stream`."""
     if jobs:
-        check(lib().kfac_factor_flush(as_array(FactorJob, jobs), len(jobs), stream_handle(device)),
+        check(lib().kfac_factor_flush(as_array(FactorJob, jobs), len(jobs),
+                                      stream_handle(device) if stream is None else stream),
               "kfac_factor_flush")
 
 

@@ -259,7 +259,13 @@ class KFAC(Curvature):
         self._fast = None        # job templates of the last slow-path update (see _remember)
         self._fast_alt = []      # this cycle's other valid templates (other batch shapes)
         self._fast_cache = {}    # packed buffer data_ptr -> templates onto its views (cycle starts)
-        self._acc_buf = None     # device buffer of the accumulators
+        # device buffers of the accumulators: two, taken in turn by cycles whose reduce
+        # ran on an inversion side stream (reduce_on_side), so the next pass writes one
+        # while that reduce still reads the other; `_acc_reads`: buffer data_ptr -> the
+        # event after its side reduce, waited for before the buffer is written again
+        self._acc_bufs = [None, None]
+        self._acc_par = 0
+        self._acc_reads = {}
         self._acc_map = None     # F pointer -> (acc pointer, splits) of the pending cycle
         self._acc_live = set()   # F pointers already written in the pending cycle
         self._acc_flush = None   # flush jobs of the pending cycle (None: nothing pending)
@@ -281,6 +287,11 @@ class KFAC(Curvature):
         # one launch for the groups of a queued flush (full batches + short last one);
         # off by default: measured neutral to 2 % slower on the MLP line
         self.merge_launches = False
+        # invert() of a pass whose reduction is still deferred runs that reduce on the
+        # inversion's side stream, ahead of the inversion, instead of on the caller's
+        # stream: the next pass's SYRK launch follows the last one directly (latency-
+        # bound inversions only, overlap_invert on)
+        self.reduce_on_side = True
         self._inv_streams = {}    # device index -> side streams
 
     def reset(self):
@@ -744,9 +755,7 @@ class KFAC(Curvature):
             for F, rs in ranges.items():
                 offs[F] = total
                 total += sum(nb for _, nb in rs)  # (bytes are linear in the splits)
-            buf = self._acc_buf
-            if buf is None or buf.device != device or buf.numel() < total:
-                buf = self._acc_buf = torch.empty(total, dtype=torch.uint8, device=device)
+            buf = self._acc_buffer(total, device)
             base = buf.data_ptr()
             self._acc_map, self._acc_live, flush = {}, set(), []
             for F, rs in ranges.items():
@@ -771,6 +780,54 @@ class KFAC(Curvature):
             j.acc_beta = 1.0 if (j.F, k) in self._acc_live else 0.0
             self._acc_live.add((j.F, k))
 
+    def _acc_buffer(self, total, device):
+        """The accumulator buffer of a new cycle (this turn's of the two), at least
+        `total` bytes; the caller's stream first waits for a side-stream reduce still
+        reading it (that wait also covers its release when it is regrown)."""
+        par = self._acc_par
+        buf = self._acc_bufs[par]
+        if buf is not None:
+            ev = self._acc_reads.pop(buf.data_ptr(), None)
+            if ev is not None:
+                if not ev.query():
+                    ev.wait_on(N.stream_handle(buf.device))
+                self._pool_event(buf.device, ev)
+        if buf is None or buf.device != device or buf.numel() < total:
+            buf = self._acc_bufs[par] = torch.empty(total, dtype=torch.uint8, device=device)
+        return buf
+
+    def _take_reduce(self):
+        """For invert(): launch the queued updates and, when the pass's reduction is
+        still deferred and can run on the inversion's side stream (reduce_on_side,
+        overlap_invert, every factor of a latency-bound size), hand back its flush jobs
+        instead of reducing on the caller's stream; else None (`state` reduces as usual)."""
+        if not (self.reduce_on_side and self.overlap_invert and self.defer_reduce):
+            return None
+        if self._queue:
+            self._launch_queue()
+        self._launch_at = self.launch_first
+        jobs = self._acc_flush
+        if not jobs or not self._state or max(F_.shape[0] for v in self._state.values() for F_ in v) > 24 * 64:
+            return None
+        self._acc_flush = self._acc_map = None
+        return jobs
+
+    def _reduce_on_side(self, jobs, device, main_h, side_h):
+        """The pass's deferred reduce on the side stream: after the caller's stream's
+        launches, after the inversion that last read the target buffer; the event after
+        it guards the accumulator buffer until the next cycle that takes it."""
+        ev = self._event(device)
+        ev.record(main_h)
+        ev.wait_on(side_h)
+        self._pool_event(device, ev)  # (the wait captured its record)
+        self._await_readers(side_h)
+        N.factor_flush(jobs, device, stream=side_h)
+        done = self._event(device)
+        done.record(side_h)
+        buf = self._acc_bufs[self._acc_par]
+        self._acc_reads[buf.data_ptr()] = done
+        self._acc_par ^= 1
+
     # ------------------------------------------------------------------ invert
     def _damping(self, add, multiply, count=None):
         """curvatures.py:373-378 argument handling, per state entry (`count`: the
@@ -789,17 +846,25 @@ class KFAC(Curvature):
 
     def invert(self, add: Union[float, list, tuple] = 0., multiply: Union[float, list, tuple] = 1.):
         """L = cholesky(inverse(sqrt(s) F + sqrt(n) I)) per factor (curvatures.py:367-398)."""
-        state = self.state  # (one flush: `state` completes the deferred reduction)
-        assert state, "State dict is empty. Did you call 'update' prior to this?"
-        # a previous inversion's verdict (deferred mode) is settled or queued here
-        self._defer_verdict()
-        if self._inv_state:
-            Warning("State has already been inverted. Is this expected?")
-        entries = list(state.items())
-        damping = self._damping(add, multiply, len(entries))
-        for layer, (first, second) in entries:
-            N.require_device(first, "state", layer)
-            N.require_device(second, "state", layer)
+        # the pass's deferred reduction: on the inversion's side stream (_take_reduce),
+        # or completed here on the caller's stream by the `state` read
+        side_reduce = self._take_reduce()
+        try:
+            state = self._state if side_reduce else self.state
+            assert state, "State dict is empty. Did you call 'update' prior to this?"
+            # a previous inversion's verdict (deferred mode) is settled or queued here
+            self._defer_verdict()
+            if self._inv_state:
+                Warning("State has already been inverted. Is this expected?")
+            entries = list(state.items())
+            damping = self._damping(add, multiply, len(entries))
+            for layer, (first, second) in entries:
+                N.require_device(first, "state", layer)
+                N.require_device(second, "state", layer)
+        except BaseException:
+            if side_reduce:  # raised before the side stream took it: reduce here after all
+                self._end_cycle(side_reduce)
+            raise
         device = entries[0][1][0].device
         # The inversion runs on a high-priority side stream (overlap_invert): its
         # critical path is a chain of single-workgroup tile factorisations, so the
@@ -828,7 +893,13 @@ class KFAC(Curvature):
         read = self._event(device) if side is not None else None
         done, order = self._event(device), self._event(device)
         host = self._pinned_host(len(jobs))
-        N.invert_pipelined(jobs, device, host, order, read, done, main_h, side_h, side)
+        after = main_h  # the stream the inversion is ordered after
+        if side_reduce:
+            if side is None or not latency_bound:  # (cannot happen: _take_reduce checked)
+                raise RuntimeError("KFAC.invert: side-stream reduce without a side stream")
+            self._reduce_on_side(side_reduce, device, main_h, side_h)
+            after = side_h
+        N.invert_pipelined(jobs, device, host, order, read, done, after, side_h, side)
         self._pool_event(device, order)  # (the side stream's wait captured its record)
         if read is not None:
             self._release(main_h, read, entries, device)

@@ -66,11 +66,13 @@ def fake_accum_plan(jobs):
 
 
 FLUSHES = []
+FLUSH_STREAMS = []  # per flush: the raw stream it was issued on (None: the caller's)
 
 
-def fake_factor_flush(jobs, device):
+def fake_factor_flush(jobs, device, stream=None):
     """kfac_factor_flush: F = beta F + alpha acc."""
     FLUSHES.append(len(jobs))
+    FLUSH_STREAMS.append(stream)
     for j in jobs:
         n = j.x.cols + j.x.has_ones
         stride = j.acc_stride or j.acc_splits

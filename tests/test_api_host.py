@@ -158,6 +158,70 @@ def test_deferred_reduce_host_logic(monkeypatch):
         np.testing.assert_allclose(g, w, rtol=1e-6)
 
 
+def test_invert_reduces_pass_on_side_stream(monkeypatch):
+    """invert() of a pass whose reduction is deferred issues that reduce on the
+    inversion's side stream (reduce_on_side), the cycles' accumulators alternate between
+    two buffers, `state` afterwards holds the reduced factors; an invert() that raises
+    before the side stream takes the reduce (bad damping) reduces on the caller's
+    stream instead, and off (reduce_on_side False) the reduce stays there."""
+    from bnn_kfac_amd import _native as N
+    from bnn_kfac_amd.curvatures import KFAC
+    host_double.install(monkeypatch)
+    monkeypatch.setattr(N, "RawEvent", host_double.HostRawEvent)
+    monkeypatch.setattr(N, "invert_pipelined", host_double.fake_invert_pipelined)
+    monkeypatch.setattr(N, "stream_handle", lambda device: 0)
+
+    class Side:
+        cuda_stream = 7
+
+    rng = np.random.default_rng(5)
+    net = mlp()
+    kfac = KFAC(net)
+    kfac._inv_streams[None] = Side()  # (a single side stream set by hand; CPU device index)
+    kfac._pinned_host = lambda n: torch.empty(n, dtype=torch.int32)
+    accs = []
+    for cycle in range(4):
+        host_double.FLUSH_STREAMS.clear()
+        kfac.reset()
+        ref = O.OracleKFAC(np.float64)
+        for B in (6, 4):
+            a1 = rng.random((B, 6), dtype=np.float32)
+            g1 = rng.standard_normal((B, 5)).astype(np.float32)
+            a2 = rng.random((B, 5), dtype=np.float32)
+            g2 = rng.standard_normal((B, 3)).astype(np.float32)
+            kfac.record[net[0]] = [torch.from_numpy(a1), torch.from_numpy(g1)]
+            kfac.record[net[2]] = [torch.from_numpy(a2), torch.from_numpy(g2)]
+            kfac.update(B)
+            ref.update_linear("l0", a1, g1, True)
+            ref.update_linear("l1", a2, g2, True)
+        accs.append(kfac._acc_map and min(a for a, _, _ in kfac._acc_map.values()))
+        if cycle == 2:
+            with pytest.raises(AssertionError):
+                kfac.invert([0.04], [200.0, 200.0])  # damping list of the wrong length
+            assert host_double.FLUSH_STREAMS == [None]  # reduced on the caller's stream
+        else:
+            kfac.invert(0.04, 200)
+            assert host_double.FLUSH_STREAMS == [7]  # the reduce went to the side stream
+        for m, name in ((net[0], "l0"), (net[2], "l1")):
+            for got, want in zip(kfac.state[m], ref.state[name]):
+                np.testing.assert_allclose(got.numpy(), want, rtol=1e-5)
+            if cycle != 2:
+                for L, F in zip(kfac.inv_state[m], kfac.state[m]):
+                    np.testing.assert_allclose(L.numpy(), O.invert_factor(F.numpy().astype(np.float64), 0.04, 200),
+                                               rtol=1e-4, atol=1e-6)
+    # accumulators alternate after a side reduce (cycles 0, 1: two buffers), and a
+    # cycle reduced on the caller's stream (2) leaves the turn where it was
+    assert accs[0] != accs[1] and accs[2] == accs[0] and accs[3] == accs[0]
+    host_double.FLUSH_STREAMS.clear()
+    kfac.reduce_on_side = False
+    kfac.reset()
+    kfac.record[net[0]] = [torch.from_numpy(a1), torch.from_numpy(g1)]
+    kfac.record[net[2]] = [torch.from_numpy(a2), torch.from_numpy(g2)]
+    kfac.update(B)
+    kfac.invert(0.04, 200)
+    assert host_double.FLUSH_STREAMS == [None]
+
+
 def test_queued_updates_merge_into_multibatch_jobs(monkeypatch):
     """update() queues; consecutive batches with matching operands become ONE
     multi-batch job per factor (K walks every queued batch), a batch of another
