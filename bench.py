@@ -562,6 +562,17 @@ def main(argv=None):
     from bnn_kfac_amd.curvatures import KFAC
     from bnn_kfac_amd.distributed import DistributedKFAC
 
+    others = None
+    if world == 1 and args.config == "mlp" and not args.no_other_configs and not args.strong:
+        # BASELINE's other single-GPU configs (C5 wide MLP, C3 LeNet-5), GPU-only, in
+        # the same run, BEFORE the headline: from an idle GPU the pipelined MLP step
+        # takes ~60 steps to settle (0.38 -> 0.34 ms per step in blocks of 20,
+        # tools/probe_warm.py, profiles/r05k/), so with these first the headline's
+        # warmup and timed steps run on a GPU that is already busy, as in training
+        others = {"C5": other_config("wide", device, steps=10, warmup=2),
+                  "C3": other_config("lenet", device, steps=20, warmup=2)}
+        torch.cuda.empty_cache()
+
     specs = CONFIGS[args.config]
     net = build_model(args.config, device)
     layers = [m for m in net.modules() if isinstance(m, (torch.nn.Linear, torch.nn.Conv2d))]
@@ -634,6 +645,34 @@ def main(argv=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t)
 
+    # The serial figure first (like the C5 / C3 legs above): the pipelined headline
+    # below is then warmed up and timed on a GPU that has been busy with this workload.
+    # From idle the GPU's clocks ramp over ~20-30 ms of it (the step 0.39 -> 0.35 ms in
+    # blocks of 20 steps; the ramp recurs after 1 s idle: profiles/r05m/), which at
+    # K = 20 steps would otherwise be most of the timed region.  The end-to-end leg
+    # (torch forward/backward GEMMs) stays after the headline: run before it, it slowed
+    # the headline's SYRK (312 vs 295 us per launch, 1.61e8 vs 1.73e8 img/s on one box,
+    # profiles/r05p/).
+    serial = None
+    if not args.no_serial:
+        # the caller who runs a pass, inverts on its own stream and reads the result
+        # before the next pass (classification_ll_block.py:93-106): no overlap
+        kfac.overlap_invert = False
+        kfac.launch_first = serial_launch_first
+        one_pass()
+        kfac.inv_state
+        sync()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            one_pass()
+            kfac.inv_state
+            torch.cuda.synchronize(device)
+        sync()
+        serial = world * images * args.steps / max_over_ranks(time.perf_counter() - t1)
+        kfac.overlap_invert = True
+        kfac.launch_first = pipe_launch_first
+
+
     for _ in range(args.warmup):
         one_pass()
     kfac.inv_state  # settle the warmup's verdicts
@@ -685,37 +724,6 @@ def main(argv=None):
         allreduce_ms = max_over_ranks(sum(a.elapsed_time(b) for a, b in comm.pop("events", []))
                                       / args.steps)
 
-    images_total = world * images * args.steps
-    value = images_total / elapsed
-    ms_per_step = 1e3 * elapsed / args.steps
-    roofline, breakdown = roofline_of(prof, specs, images, args.steps, args.config)
-    breakdown.update({"allreduce_ms_per_step": allreduce_ms,
-                      "host_issue_ms_per_step": 1e3 * t_issue / args.steps,
-                      "updates_per_step": len(starts)})
-
-    serial = None
-    if not args.no_serial:
-        # the caller who runs a pass, inverts on its own stream and reads the result
-        # before the next pass (classification_ll_block.py:93-106): no overlap
-        kfac.overlap_invert = False
-        kfac.launch_first = serial_launch_first
-        one_pass()
-        kfac.inv_state
-        sync()
-        t1 = time.perf_counter()
-        for _ in range(args.steps):
-            one_pass()
-            kfac.inv_state
-            torch.cuda.synchronize(device)
-        sync()
-        serial = world * images * args.steps / max_over_ranks(time.perf_counter() - t1)
-        kfac.overlap_invert = True
-        kfac.launch_first = pipe_launch_first
-
-    parity = None
-    if world > 1 and not args.no_parity:
-        parity = verify_parity(kfac, net, specs, recs, batch, images, world, rank, device, sync)
-
     e2e = None
     if not args.no_e2e and world == 1:
         x = torch.rand(images, *specs[0].in_shape, device=device)
@@ -743,16 +751,21 @@ def main(argv=None):
         kfac.inv_state
         sync()
         e2e = images * reps / (time.perf_counter() - t1)
+        del x
 
-    others = None
-    if world == 1 and args.config == "mlp" and not args.no_other_configs and not args.strong:
-        # BASELINE's other single-GPU configs, GPU-only, in the same run (the records of
-        # the headline pass are freed first)
-        del views, recs
-        record.clear()
-        torch.cuda.empty_cache()
-        others = {"C3": other_config("lenet", device, steps=20, warmup=2),
-                  "C5": other_config("wide", device, steps=10, warmup=2)}
+    images_total = world * images * args.steps
+    value = images_total / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+    roofline, breakdown = roofline_of(prof, specs, images, args.steps, args.config)
+    breakdown.update({"allreduce_ms_per_step": allreduce_ms,
+                      "host_issue_ms_per_step": 1e3 * t_issue / args.steps,
+                      "updates_per_step": len(starts)})
+
+
+    parity = None
+    if world > 1 and not args.no_parity:
+        parity = verify_parity(kfac, net, specs, recs, batch, images, world, rank, device, sync)
+
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
