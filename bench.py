@@ -319,12 +319,14 @@ def verify_parity(kfac, net, specs, recs, batch, images, world, rank, device, sy
 
 
 def load_traffic(config):
+    """The committed PMC profile of `config`'s dominant factor kernel (profiles/
+    summarize.py): {kernel, tag, hbm_bytes_per_launch, ...}, or None."""
     name = "factor_tiles_pmc.json" if config == "mlp" else f"factor_tiles_pmc_{config}.json"
     path = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(path):
         return None
     with open(path) as f:
-        return json.load(f).get("hbm_bytes_per_launch")
+        return json.load(f)
 
 
 def profiled_steps(N, one_pass, kfac, sync, steps):
@@ -359,9 +361,17 @@ def roofline_of(prof, specs, images, steps, config):
     flops_timed = fpi * images * steps
     achieved = flops_timed / (tiles_ms * 1e-3) / 1e12 if tiles_ms > 0 else None
     peak = SYRK3_PEAK_TFLOPS if syrk3 else MFMA_F32_PEAK_TFLOPS
+    # traffic: HBM bytes per launch of the same kernel from the committed rocprofv3 PMC
+    # passes of this config's single-GPU bench launch (null when the profile is of
+    # another kernel)
+    pmc = load_traffic(config)
+    pmc_ok = pmc is not None and pmc.get("kernel") == prod_kernel
     roofline = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                 "frac": (achieved / peak) if achieved else None,
-                "traffic": load_traffic(config),
+                "traffic": pmc.get("hbm_bytes_per_launch") if pmc_ok else None,
+                "traffic_source": (f"profiles/{pmc.get('tag')}/: rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
+                                   f"mean per {prod_kernel} launch of the single-GPU {config} bench")
+                                  if pmc_ok else None,
                 "kernel": prod_kernel,
                 # (the same rate against the fp32 MFMA peak, the basis of earlier rounds)
                 "frac_fp32_peak_basis": (achieved / MFMA_F32_PEAK_TFLOPS) if achieved else None,
