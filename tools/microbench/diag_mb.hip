@@ -22,10 +22,6 @@ __global__ __launch_bounds__(256) void mb(const double* src, double* dst, int re
     if (MODE == 3) diag_factor<1>(S, Y, dg);
     if (MODE == 4) diag_factor<6>(S, Y, dg);
     if (MODE == 5) diag_factor<0>(S, Y, dg);
-    if (MODE == 6) diag_factor<7, true>(S, Y, dg);  // register-only elimination (elim_col)
-    if (MODE == 7) diag_factor<1, true>(S, Y, dg);
-    if (MODE == 8) diag_factor<7, false, true>(S, Y, dg);  // 4 columns per LDS exchange
-    if (MODE == 9) diag_factor<1, false, true>(S, Y, dg);
     if (MODE == 1) {  // load + barrier only
       for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) Y[(e >> 6) * DP + (e & 63)] = S[(e >> 6) * DP + (e & 63)];
     }
@@ -79,11 +75,7 @@ int main() {
   printf("diag elim only %8.2f us/rep\n", run<3>(s, d, reps));
   printf("diag mfma only %8.2f us/rep\n", run<4>(s, d, reps));
   printf("diag skeleton  %8.2f us/rep\n", run<5>(s, d, reps));
-  printf("diag elim only (xlane) %8.2f us/rep\n", run<7>(s, d, reps));
-  printf("diag_factor (xlane)    %8.2f us/rep\n", run<6>(s, d, reps));
   printf("diag_factor    %8.2f us/rep\n", run<0>(s, d, reps));
-  printf("diag elim only (blk4)  %8.2f us/rep\n", run<9>(s, d, reps));
-  printf("diag_factor (blk4)     %8.2f us/rep\n", run<8>(s, d, reps));
   // correctness: Y * chol(S) == I  ->  check (Y S Y^T) == I
   std::vector<double> y(NB * NB);
   (void)hipMemcpy(y.data(), d, sizeof(double) * NB * NB, hipMemcpyDeviceToHost);
