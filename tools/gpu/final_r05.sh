@@ -2,7 +2,7 @@
 # the kernel trace of the bench's headline loop
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r05_end
+O=gpurun_out/r05_end2
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
 tail -2 $O/gpu_tests.log
