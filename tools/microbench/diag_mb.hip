@@ -25,9 +25,10 @@ __global__ __launch_bounds__(256) void mb(const double* src, double* dst, int re
     if (MODE == 1) {  // load + barrier only
       for (int e = threadIdx.x; e < NB * NB; e += NTHREADS) Y[(e >> 6) * DP + (e & 63)] = S[(e >> 6) * DP + (e & 63)];
     }
-    if (MODE == 2) {  // 64x64x64 MFMA gemm only
+    if (MODE == 2 || MODE == 6) {  // 64x64x64 MFMA gemm only (6: B not transposed)
       doublex4 acc[4];
-      gemm64<true>(S, S, acc);
+      if (MODE == 2) gemm64<true>(S, S, acc);
+      else gemm64<false>(S, S, acc);
       const int w = threadIdx.x >> 6, col = threadIdx.x & 15;
       for (int b4 = 0; b4 < 4; ++b4)
         for (int v = 0; v < 4; ++v) Y[(16 * w + acc_row64(v)) * DP + 16 * b4 + col] = acc[b4][v];
@@ -72,6 +73,7 @@ int main() {
   const int reps = 200;
   printf("load+copy      %8.2f us/rep\n", run<1>(s, d, reps));
   printf("gemm64 f64     %8.2f us/rep\n", run<2>(s, d, reps));
+  printf("gemm64 f64 nn  %8.2f us/rep\n", run<6>(s, d, reps));
   printf("diag elim only %8.2f us/rep\n", run<3>(s, d, reps));
   printf("diag mfma only %8.2f us/rep\n", run<4>(s, d, reps));
   printf("diag skeleton  %8.2f us/rep\n", run<5>(s, d, reps));
