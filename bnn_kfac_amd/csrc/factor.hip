@@ -38,7 +38,6 @@ struct FactorJobDev {
   int tile_begin;    // first global tile of this job (reduce launch)
   int accum;         // deferred reduction: `slab` is the caller's accumulator
   float sbeta;       // accumulator update: slab = sbeta*slab + alpha*partial
-  char* split3;      // pre-split bf16x3 panel images of the job (kfac_factor_syrk3), else null
   int x3pair;        // kfac_factor_tiles_x3: thin last tile row, diagonal + edge tiles paired
   int sstride;       // slabs per tile of `slab` (a job's split s of tile t: t * sstride + s)
   int xsplits;       // x3 thin-row pairs: of the `splits` slabs per tile, the last xsplits are
@@ -494,17 +493,12 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
 // (v_mfma_f32_32x32x2_f32), so six of them are 2.67x the fp32 MFMA rate: the
 // roofline of this kernel is 2.5 PF / 6 = 417 TF/s of fp32-equivalent work.
 //
-// Two launches per grouped update:
-//   kfac_split3        streams each 32-row stage of each 128-column panel of the
-//                      operand ONCE into its three bf16 parts, laid out byte for byte
-//                      as the SYRK's LDS image of that panel (HBM-bound, 4 B read +
-//                      6 B written per element);
-//   kfac_factor_syrk3  one 128 x 128 macro tile (= 2 x 2 of the 64-tiles whose
-//                      partial slabs the reduce sums) of one factor over one K-chunk
-//                      per workgroup: wave w computes the 64 x 64 quadrant (w >> 1,
-//                      w & 1) as 2 x 2 blocks of 32 x 32; the panel images arrive by
-//                      LDS-DMA (global_load_lds_dwordx4) into a ring of 16-row
-//                      k-substeps -- no staging registers, no VALU in the loop.
+// kfac_factor_syrk3: one 128 x 128 macro tile (= 2 x 2 of the 64-tiles whose partial
+// slabs the reduce sums) of one factor over one K-chunk per workgroup; the workgroup
+// loads each 16-row substep of its panels once, splits it into the LDS image below and
+// its 4 waves multiply from there (s3q_task).  Until round 5 a separate kfac_split3
+// pass wrote the split images to HBM (6 B per operand element) and the SYRK read them
+// back by LDS-DMA.
 // LDS image of a substep: [part][column][2 chunks of 8 k] (32 B per column, k
 // contiguous), read straight into MFMA operands (lane = column, 8 k per
 // ds_read_b128); the chunk of a column is XOR-swizzled by bit 3 of the column, so the
@@ -608,70 +602,36 @@ __device__ __forceinline__ void s3_decode(int unit, int T3, int& I, int& J) {
   }
 }
 
-// ------------------------------------------- bf16x3 SYRK: split pass and SYRK
-// The ring: NSLOT single-substep slots (24,640 B each) per workgroup, NSLOT - 1 in
-// flight, one barrier per substep; S3D_WGS workgroups per CU (256 threads, one wave
-// per SIMD each) interleave their barriers and DMA waits.  2 slots x 3 workgroups
-// measured best on the wide C5 line.
-constexpr int S3_PANEL = 2 * 3 * MT * 32;  // bytes of one panel's split stage (24 KB)
-#ifndef KFAC_S3D_NSLOT
-#define KFAC_S3D_NSLOT 2  // (compile-time: the ring-depth A/B builds)
-#endif
+// ------------------------------------- bf16x3 SYRK, split once per workgroup
+// (round 5; replaces the separate split pass).  One 128 x 128 macro
+// tile of one factor over one K-chunk per workgroup of 4 waves, 2 workgroups per CU.
+// Per 16-row substep, thread t loads column t of the [A panel | B panel] (256 columns)
+// -- 16 rows, two 8-row halves, buffer loads whose record limit zero-fills rows past
+// the batch and columns past the operand -- splits it into its three bf16 parts and
+// writes them as the substep's LDS image (the layout above: [part][column][2 halves],
+// half swizzled by bit 3 of the column).  Two slots: while the waves' MFMAs consume
+// substep h from one, the split of substep h + 1 goes into the other, interleaved with
+// those MFMAs (sched_group_barrier), and the loads of substep h + 2 are in flight.
+// One barrier per substep.  Each wave computes its 64 x 64 quadrant (w >> 1, w & 1)
+// as 2 x 2 blocks, six products per block: 24 MFMAs per substep against 2 columns x
+// 16 values split per thread (3.7 VALU per MFMA; tools/microbench/cutq_mb.hip: 0.448
+// of 417 TF/s on a 4096-column operand).
 #ifndef KFAC_S3D_WGS
-#define KFAC_S3D_WGS 3  // resident workgroups per CU the planner counts on
+#define KFAC_S3D_WGS 2  // resident workgroups per CU the planner counts on
 #endif
-constexpr int S3D_NSLOT = KFAC_S3D_NSLOT;
 constexpr int S3D_WGS = KFAC_S3D_WGS;
-constexpr int S3D_LDS = S3D_NSLOT * S3_REG;
+constexpr int S3D_LDS = 2 * S3_REG;
 
-// one (stage, panel) of one job per workgroup: thread (c = t & 127, h = t >> 7) takes
-// column c's rows 8h .. 8h+7 (region 0) and 16 + 8h .. (region 1)
-__global__ __launch_bounds__(NTHREADS) void kfac_split3(FactorArgs args) {
-  const int task = blockIdx.x;
-  int j = 0;
-  while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
-  const FactorJobDev& J = args.job[j];
-  const int T3 = (J.n + MT - 1) / MT;
-  const int local = task - J.task_begin;
-  const int64_t st = local / T3;
-  const int panel = local - (int)st * T3;
-  const int seg = (int)(st / J.sps);
-  const int64_t k0 = (st - (int64_t)seg * J.sps) * BK;
-  const float* base = seg_base(J, args.segs, seg);
-  const int ld = (int)J.x.ld;
-  const int nrow = (int)min((int64_t)BK, J.x.rows - k0);
-  const int c = threadIdx.x & 127, h = threadIdx.x >> 7;
-  const int col = panel * MT + c;
-  const bool real = col < J.x.cols, ones = col == J.x.ones;
-  char* out = J.split3 + ((size_t)st * T3 + panel) * S3_PANEL;
-#pragma unroll
-  for (int reg = 0; reg < 2; ++reg) {
-    const int r0 = 16 * reg + 8 * h;
-    float v[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int row = r0 + r;
-      v[r] = row < nrow ? (real ? base[(k0 + row) * ld + col] : (ones ? 1.f : 0.f)) : 0.f;
-    }
-    uint32_t p0[4], p1[4], p2[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) split3(v[2 * i], v[2 * i + 1], p0[i], p1[i], p2[i]);
-    char* d = out + reg * 3 * MT * 32 + s3_half(c, h);
-    *reinterpret_cast<uint4*>(d) = make_uint4(p0[0], p0[1], p0[2], p0[3]);
-    *reinterpret_cast<uint4*>(d + MT * 32) = make_uint4(p1[0], p1[1], p1[2], p1[3]);
-    *reinterpret_cast<uint4*>(d + 2 * MT * 32) = make_uint4(p2[0], p2[1], p2[2], p2[3]);
-  }
-}
-
-__device__ __forceinline__ void s3d_task(const FactorJobDev& J, int local, char* lds) {
+template <bool FILL>
+__device__ __forceinline__ void s3q_task(const FactorJobDev& J, const float* const* segs, int local,
+                                         char* lds) {
   const int T3 = (J.n + MT - 1) / MT, units = T3 * (T3 + 1) / 2;
   const int split = local / units, unit = local - split * units;
   int I, Jc;
   s3_decode(unit, T3, I, Jc);
-  const bool same = I == Jc;
   const int64_t s0 = (int64_t)split * J.chunk;
   const int64_t s1 = min(J.nst, s0 + J.chunk);
-  const int ns = (int)(s1 - s0);
+  const int nh = 2 * (int)(s1 - s0);  // 16-row substeps (even)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 1, wc = wave & 1;
@@ -683,7 +643,6 @@ __device__ __forceinline__ void s3d_task(const FactorJobDev& J, int local, char*
       const int r0 = I * MT + wr * 64 + bi * 32, c0 = Jc * MT + wc * 64 + bj * 32;
       act[bi][bj] = r0 < J.n && c0 < J.n && r0 >= c0;
     }
-  const bool any = act[0][0] || act[0][1] || act[1][0] || act[1][1];
   floatx16 acc[2][2];
 #pragma unroll
   for (int bi = 0; bi < 2; ++bi)
@@ -691,43 +650,138 @@ __device__ __forceinline__ void s3d_task(const FactorJobDev& J, int local, char*
     for (int bj = 0; bj < 2; ++bj)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[bi][bj][v] = 0.f;
-  const int cl = lane & 31, lo = s3_half(cl, lane >> 5);
-  const int oa = wr * 64 * 32 + lo;
-  const int ob = ((same ? 0 : MT) + wc * 64) * 32 + lo;
-  // DMA of one substep h (region h & 1 of stage s0 + h / 2): per panel 3 parts of
-  // 4 KB = 12 wave instructions of 1 KB; wave w takes instructions w, w + 4, w + 8
-  const char* pa = J.split3 + (size_t)I * S3_PANEL;
-  const char* pb = J.split3 + (size_t)Jc * S3_PANEL;
-  const size_t sstride = (size_t)T3 * S3_PANEL;
-  auto issue = [&](int hs) {
-    char* slot = lds + (hs % S3D_NSLOT) * S3_REG;
-    const size_t so = (size_t)(s0 + (hs >> 1)) * sstride + (size_t)(hs & 1) * 3 * MT * 32;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int i = wave + 4 * q;         // 0 .. 11
-      const int part = i >> 2, kb = i & 3;  // part, its 1 KB piece
-      const int go = part * (MT * 32) + kb * 1024;
-      const int lo_ = part * S3_PART + kb * 1024;
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(pa + so + go + lane * 16),
-                                       slot + lo_, 16, 0, 0);
-      if (!same)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(pb + so + go + lane * 16),
-                                         slot + lo_ + MT * 32, 16, 0, 0);
-    }
+  // this thread's column of the [A | B] panels
+  const int ld4 = (int)J.x.ld * 4;
+  const int rows = (int)J.x.rows;
+  const int rec = rows * ld4;  // a batch's bytes (planner: < 2^31)
+  const int gc = tid < MT ? I * MT + tid : Jc * MT + (tid - MT);
+  const int voff = gc < J.x.cols ? gc * 4 : rec;  // past the operand: the zero tail
+  const bool ones = gc == J.x.ones;
+  const int wo = s3_half(tid, 0), wo1 = s3_half(tid, 1);
+  // substep cursor: batch `seg` (base `b`), first row `k` of the substep within it
+  const int sub_per_seg = 2 * J.sps;
+  int seg = (int)(s0 / J.sps);
+  int k = (int)((s0 - (int64_t)seg * J.sps) * BK);
+  const int lastseg = J.nseg - 1;
+  const float* b = seg_base(J, segs, seg);
+  const float* nb = seg_base(J, segs, min(seg + 1, lastseg));  // the next batch's base
+  int left = nh - 1;  // substeps after the cursor's within the task (it stops at the last)
+  int ksub = k / 16;  // substep index within the batch
+  // branch-free (scalar selects): a branch here splits the loop body and the compiler
+  // then copies the load register sets at the join
+  auto advance = [&]() {
+    const int more = left > 0;
+    left -= more;
+    ksub += more;
+    k += 16 * more;
+    const bool wrap = ksub == sub_per_seg;
+    ksub = wrap ? 0 : ksub;
+    k = wrap ? 0 : k;
+    seg += wrap;
+    b = wrap ? nb : b;
+    nb = seg_base(J, segs, min(seg + 1, lastseg));
   };
-  const int per = same ? 3 : 6;  // DMA instructions per wave per substep
-  const int nh = 2 * ns;          // substeps of the task
-  if (nh > 0) {
+  struct Sub {
+    int seg, k;
+  };
+  auto load = [&](float (&L)[2][8]) {
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(b), 0, rec, 0x00020000);
 #pragma unroll
-    for (int p0 = 0; p0 < S3D_NSLOT - 1; ++p0)
-      if (p0 < nh) issue(p0);
-    for (int hs = 0; hs < nh; ++hs) {
-      const int issued = min(nh - 1, hs + S3D_NSLOT - 2);  // last substep already issued
-      vm_wait(per * (issued - hs));
-      stage_barrier();  // substep hs landed for every wave; the slot of hs - 1 is free
-      if (hs + S3D_NSLOT - 1 < nh) issue(hs + S3D_NSLOT - 1);
-      if (any) s3_consume_sub(lds + (hs % S3D_NSLOT) * S3_REG, oa, ob, act, acc);
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        L[u][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, (k + 8 * u + r) * ld4, 0));
+  };
+  auto put1 = [&](float (&x)[8], int u, const Sub& sb, char* slot) {
+    if constexpr (FILL) {  // the ones column: 1 on the batch's rows, 0 past them
+      const int nvalid = (int)seg_rows(J, sb.seg) - sb.k - 8 * u;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) x[r] = ones ? (r < nvalid ? 1.f : 0.f) : x[r];
     }
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 hp, mp, lp;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint32_t a2, b2, c2;
+      split3(x[2 * i], x[2 * i + 1], a2, b2, c2);
+      hp[i] = a2;
+      mp[i] = b2;
+      lp[i] = c2;
+    }
+    const int o = u ? wo1 : wo;
+    *reinterpret_cast<u32x4*>(slot + o) = hp;
+    *reinterpret_cast<u32x4*>(slot + S3_PART + o) = mp;
+    *reinterpret_cast<u32x4*>(slot + 2 * S3_PART + o) = lp;
+  };
+  const int lo = s3_half(lane & 31, lane >> 5);
+  const int oa = wr * 64 * 32 + lo, ob = (MT + wc * 64) * 32 + lo;
+  auto frag = [&](const char* slot, int off) { return *reinterpret_cast<const bf16x8*>(slot + off); };
+  float L0[2][8], L1[2][8];
+  Sub sub0{seg, k}, sub1;
+  load(L0);
+  advance();
+  sub1 = Sub{seg, k};
+  load(L1);
+  advance();
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // L0 landed
+  put1(L0[0], 0, sub0, lds);
+  put1(L0[1], 1, sub0, lds);
+  __syncthreads();
+  // substep hs: MFMAs from slot hs & 1; Lsplit (substep hs + 1) split into the other
+  // slot during them; Lload refilled with substep hs + 2
+  auto body = [&](int hs, float (&Lsplit)[2][8], const Sub& ssplit, float (&Lload)[2][8]) {
+    const char* cur = lds + (hs & 1) * S3_REG;
+    char* nxt = lds + ((hs + 1) & 1) * S3_REG;
+    bf16x8 A[2][3], B[2][3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) A[0][p] = frag(cur, oa + p * S3_PART);
+    load(Lload);  // (past the task's rows: the last substep again, never used)
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // Lsplit has landed
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi) {
+      if (bi == 0)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) A[1][p] = frag(cur, oa + p * S3_PART + 32 * 32);
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj) {
+        if (bi == 0)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) B[bj][p] = frag(cur, ob + p * S3_PART + bj * 32 * 32);
+        const bf16x8* Aa = A[bi];
+        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Aa[2], B[bj][0], acc[bi][bj], 0, 0, 0);
+        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Aa[1], B[bj][1], acc[bi][bj], 0, 0, 0);
+        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Aa[0], B[bj][2], acc[bi][bj], 0, 0, 0);
+        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Aa[1], B[bj][0], acc[bi][bj], 0, 0, 0);
+        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Aa[0], B[bj][1], acc[bi][bj], 0, 0, 0);
+        acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Aa[0], B[bj][0], acc[bi][bj], 0, 0, 0);
+      }
+      // (unconditional: past the last substep it fills the free slot -- a branch here
+      // made the compiler copy the 64 accumulators every trip)
+      put1(Lsplit[bi], bi, ssplit, nxt);
+      // pattern: the fragment reads first, then per MFMA ~4 VALU of the split, a DS
+      // write every 4 MFMAs
+      if (bi == 0) __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+      for (int i = 0; i < 12; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (bi == 0 && i == 5) __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+        if (i % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+  };
+  for (int hs = 0; hs < nh; hs += 2) {
+    const Sub s2{seg, k};
+    body(hs, L1, sub1, L0);  // L0 <- substep hs + 2
+    advance();
+    sub0 = s2;
+    const Sub s3{seg, k};
+    body(hs + 1, L0, sub0, L1);  // L1 <- substep hs + 3
+    advance();
+    sub1 = s3;
   }
   const int ti = 2 * I + wr, tj = 2 * Jc + wc;
   float* o = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.sstride + split) * TILE * TILE;
@@ -747,10 +801,20 @@ __global__ __launch_bounds__(NTHREADS, S3D_WGS) void kfac_factor_syrk3(FactorArg
   while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
   const FactorJobDev& J = args.job[j];
   const int local = task - J.task_begin;
-  if (J.n <= 32)
+  if (J.n <= 32) {
     factor_task_narrow_direct(J, args.segs, local, reinterpret_cast<float*>(s3lds));
+    return;
+  }
+  // the macro tile whose panels hold the ones column splits with the fill
+  const int T3 = (J.n + MT - 1) / MT, units = T3 * (T3 + 1) / 2;
+  int I, Jc;
+  s3_decode(local % units, T3, I, Jc);
+  const int o = J.x.ones;
+  const bool fill = o >= 0 && (o / MT == I || o / MT == Jc);
+  if (fill)
+    s3q_task<true>(J, args.segs, local, s3lds);
   else
-    s3d_task(J, local, s3lds);
+    s3q_task<false>(J, args.segs, local, s3lds);
 }
 
 // ------------------------------- fp32 operands, bf16x3 products split in registers
@@ -2000,12 +2064,6 @@ static int syrk3_mode() {
 }
 
 // bytes of a job's pre-split panel images (kfac_factor_syrk3; narrow jobs: none)
-static size_t split3_bytes(const kfac_factor_job& j) {
-  const int n = factor_n(j);
-  if (n <= 32) return 0;
-  const int64_t t3 = cdiv(n, MT);
-  return align_up((size_t)job_stages(j) * (size_t)t3 * S3_PANEL, 256);
-}
 
 static bool syrk3_group(const kfac_factor_job* jobs, int njobs) {
   const int mode = syrk3_mode();
@@ -2053,7 +2111,7 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
                       int64_t slots = 0) {
   const bool s3 = syrk3_group(jobs, njobs);
   // resident workgroups per CU: 4 (32 KB of LDS each; kfac_factor_tiles_x3: 4 of two
-  // waves -- 3 or 2 measured slower); the bf16x3 kernel: S3D_WGS (49 KB each)
+  // waves -- 3 or 2 measured slower); kfac_factor_syrk3: S3D_WGS (49 KB each)
   if (slots <= 0) slots = (s3 ? S3D_WGS : 4) * 256;
   constexpr int64_t MIN_CHUNK = 8, OVERHEAD = 4;  // stages; ~per-task fixed cost in stages
   int64_t max_steps = 1;
@@ -2102,9 +2160,11 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
   // x3 groups keep the cost model's choice, which nothing measured against)
   bool any_thin = false;
   for (int i = 0; i < njobs && x3; ++i) any_thin |= x3_thin(factor_n(jobs[i]), (int)cdiv(factor_n(jobs[i]), TILE));
-  const int64_t max_rounds = any_thin ? 1 : 4;
-  for (int64_t r = 1; r <= 4; ++r) {
-    if (r > max_rounds) continue;
+  // (kfac_factor_syrk3 groups, 2 workgroups per CU: up to 16 rounds, so a launch of
+  // ~2,200 macro tiles (wide C5) can take 2 K-splits at 9 rounds instead of 1 at 4.3:
+  // 1.61 vs 1.71 ms per launch, profiles/r05ac/)
+  const int64_t max_rounds = any_thin ? 1 : (s3 ? 16 : 4);
+  for (int64_t r = 1; r <= max_rounds; ++r) {
     int64_t lo = MIN_CHUNK, hi = std::max(MIN_CHUNK, max_steps);
     if (tasks_at(hi) > r * slots) continue;  // even one split per tile needs more rounds
     while (lo < hi) {
@@ -2215,8 +2275,8 @@ static void launch_reduce(FactorArgs& r, int tiles, hipStream_t stream) {
 // workgroups) and the reduce of the jobs without an accumulator (`red`, `rtiles`
 // tiles).  Returns KFAC_EWORKSPACE when the slabs do not fit.
 struct GroupLaunch {
-  FactorArgs args, red, split;
-  int tasks, rtiles, split_tasks;
+  FactorArgs args, red;
+  int tasks, rtiles;
 };
 
 static int prepare_group(const kfac_factor_job* jobs_in, int njobs, char* ws, size_t ws_bytes,
@@ -2267,23 +2327,6 @@ static int prepare_group(const kfac_factor_job* jobs_in, int njobs, char* ws, si
   }
   g.tasks = tasks;
   g.rtiles = rtiles;
-  g.split_tasks = 0;
-  if (syrk3_group(jobs, njobs)) {
-    // the pre-split images after the slabs; the split launch's own task ranges
-    g.split = args;
-    int st = 0;
-    for (int i = 0; i < njobs; ++i) {
-      const size_t b = split3_bytes(jobs[i]);
-      args.job[i].split3 = b ? ws + off : nullptr;
-      off += b;
-      FactorJobDev& e = g.split.job[i];
-      e.split3 = args.job[i].split3;
-      e.task_begin = st;
-      if (b) st += (int)(job_stages(jobs[i]) * cdiv(factor_n(jobs[i]), MT));
-      g.split.task_end[i] = st;
-    }
-    g.split_tasks = st;
-  }
   return off > ws_bytes ? KFAC_EWORKSPACE : KFAC_OK;
 }
 
@@ -2326,10 +2369,6 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
                 reinterpret_cast<const void*>(&kfac_factor_syrk3),
                 hipFuncAttributeMaxDynamicSharedMemorySize, S3D_LDS) == hipSuccess;
             if (!attr) return KFAC_ELAUNCH;
-            if (g.split_tasks > 0) {
-              hipLaunchKernelGGL(kfac_split3, dim3(g.split_tasks), dim3(NTHREADS), 0, stream, g.split);
-              KFAC_CHECK_LAUNCH();
-            }
             hipLaunchKernelGGL(kfac_factor_syrk3, dim3(tasks), dim3(NTHREADS), S3D_LDS, stream, args);
           } else if (x3)
             hipLaunchKernelGGL(kfac_factor_tiles_x3, dim3(tasks), dim3(X3_THREADS), 0, stream, args);
@@ -2351,8 +2390,6 @@ static size_t group_ws(const kfac_factor_job* jobs, int njobs) {
   plan_jobs(jobs, njobs, plans);
   size_t off = 0;
   for (int i = 0; i < njobs; ++i) off += plans[i].slab_bytes;
-  if (syrk3_group(jobs, njobs))
-    for (int i = 0; i < njobs; ++i) off += split3_bytes(jobs[i]);
   return off;
 }
 

@@ -20,12 +20,20 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef WIDE
 constexpr int K = 61440, LD = 784;
+#else
+constexpr int K = 16384, LD = 4096;
+#endif
 constexpr int CT = 128;           // workgroup tile edge
 constexpr int NP = 2 * CT;        // panel columns per stage (A | B)
 constexpr int PART = NP * 32;     // one part of a stage: NP cols x 16 k x 2 B
 constexpr int STG = 3 * PART;     // one stage buffer (24 KB)
+#ifndef WIDE
 constexpr int NTILE = 12;         // 128-tiles of the 256-tiles (1,0) (2,0) (2,1)
+#else
+constexpr int NTILE = 32 * 33 / 2;  // every lower-triangle 128-tile of 4096 columns
+#endif
 
 #define CHECK(x)                                                                 \
   do {                                                                           \
@@ -56,9 +64,16 @@ __device__ __forceinline__ void split3(float a, float b, uint32_t& h, uint32_t& 
 }
 // 128-tile t: 256-tile (1,0) (2,0) (2,1) by t / 4, quadrant (t % 4) / 2, t % 2
 __device__ __host__ inline void tile_cols(int t, int& ca, int& cb) {
+#ifndef WIDE
   const int T = t / 4, I = T == 0 ? 1 : 2, J = T == 2 ? 1 : 0;
   ca = I * 256 + ((t % 4) / 2) * CT;
   cb = J * 256 + (t % 2) * CT;
+#else
+  int i = 0;
+  while ((i + 1) * (i + 2) / 2 <= t) ++i;
+  ca = i * CT;
+  cb = (t - i * (i + 1) / 2) * CT;
+#endif
 }
 
 #define SB() __builtin_amdgcn_sched_barrier(0)
@@ -210,13 +225,21 @@ int main() {
   float* X;
   CHECK(hipMalloc(&X, h.size() * 4));
   CHECK(hipMemcpy(X, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+#ifndef WIDE
   const int splits = 40;  // 480 tasks: two workgroups per CU, one round
+#else
+  const int splits = 2;   // 1056 tasks
+#endif
   float* slab;
   const size_t slab_bytes = (size_t)NTILE * splits * CT * CT * 4;
   CHECK(hipMalloc(&slab, slab_bytes));
   double* ref;
   CHECK(hipMalloc(&ref, CT * CT * 8));
+#ifndef WIDE
   const int RT = 7;  // checked tile
+#else
+  const int RT = 100;
+#endif
   int rca, rcb;
   tile_cols(RT, rca, rcb);
   hipLaunchKernelGGL(k_ref, dim3(CT), dim3(CT), 0, 0, X, rca, rcb, ref);
