@@ -2073,6 +2073,8 @@ static bool syrk3_group(const kfac_factor_job* jobs, int njobs) {
     if (jobs[i].x.layout != KFAC_ROWMAJOR) return false;
     const int n = factor_n(jobs[i]);
     if (n > 32 && !job_glds(jobs[i])) return false;
+    // (buffer loads: a batch's bytes are one 31-bit record range)
+    if (n > 32 && jobs[i].x.rows * jobs[i].x.ld * (int64_t)sizeof(float) >= ((int64_t)1 << 31)) return false;
     nmax = std::max(nmax, n);
   }
   return nmax > 32 && (mode == 1 || nmax >= 2048);
