@@ -241,10 +241,11 @@ class KFAC(Curvature):
         # frees them after each update): the queue is also launched once the records
         # it holds reach this many bytes, so a wide or conv model's activations are
         # not retained beyond ~this much (MLP batch of 4096: 17 MB per update; LeNet-5
-        # batch of 1024: ~35 MB; the wide MLP: 281 MB, one update per launch).  1 GiB
-        # measured +6.6 % on LeNet-5 but -8 % on the wide MLP (3-update split-pass
-        # launches): 256 MiB stays
-        self.defer_bytes = 256 << 20
+        # batch of 1024: ~35 MB; the wide MLP: 281 MB, one update per launch).  Round 5,
+        # same box: 512 MiB +4 % on LeNet-5 (14 updates per launch instead of 7), wide
+        # unchanged (still one per launch); 1 GiB +6 % on LeNet-5 but -1.6 % on the wide
+        # MLP (3-update launches)
+        self.defer_bytes = 512 << 20
         self._queue_bytes = 0
         self._queue = []         # per queued update: (jobs, operand pointers, kept records,
                                  # their _version, device, merge key)
