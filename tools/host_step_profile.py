@@ -96,6 +96,23 @@ def main():
         one_pass()
     dt = (time.perf_counter() - t0) / steps * 1e6
     print(f"{config}: {dt:.1f} us of host time per step ({len(starts)} updates + invert)")
+    if "--phases" in sys.argv:
+        ph = [0.0, 0.0, 0.0]
+        for _ in range(steps):
+            t0 = time.perf_counter()
+            kfac.reset()
+            t1 = time.perf_counter()
+            for bv, size in zip(views, sizes):
+                for layer, rec in bv:
+                    record[layer] = rec
+                kfac.update(batch_size=size)
+            t2 = time.perf_counter()
+            kfac.invert(*bench.DAMPING)
+            t3 = time.perf_counter()
+            ph[0] += t1 - t0
+            ph[1] += t2 - t1
+            ph[2] += t3 - t2
+        print("reset / updates / invert: " + " / ".join(f"{1e6 * v / steps:.1f}" for v in ph) + " us per step")
     if "--cprofile" in sys.argv:
         pr = cProfile.Profile()
         pr.enable()

@@ -4,7 +4,7 @@ device sync as the bench's timed region is).  Per block: ms/step, the host's iss
 step (and its median one_pass call), and the caching allocator's segment allocations
 (hipMalloc calls) made inside it.
 
-    python tools/probe_warm.py [W] [K] [blocks] [pre_s] [prof|noprof] [idle_s]
+    python tools/probe_warm.py [W] [K] [blocks] [pre_s] [prof|noprof] [idle_s] [legs|legs+serial]
 
 pre_s > 0: first keep the GPU busy with unrelated work (bf16 GEMMs) for that long, to
 tell a power/clock ramp (then block 0 is already fast) from a warm-up of this code.
@@ -55,6 +55,22 @@ def main():
     def segs():
         return torch.cuda.memory_stats(dev).get("segment.all.allocated", 0)
 
+    # "legs": the bench's C5 / C3 legs first; "legs+serial": then 20 serial passes, as
+    # bench.py orders them before the headline
+    mode = sys.argv[7] if len(sys.argv) > 7 else ""
+    if mode.startswith("legs"):
+        bench.other_config("wide", dev, steps=10, warmup=2)
+        bench.other_config("lenet", dev, steps=20, warmup=2)
+        torch.cuda.empty_cache()
+    if mode == "legs+serial":
+        kfac.overlap_invert = False
+        kfac.launch_first = 1
+        for _ in range(21):
+            one_pass()
+            kfac.inv_state
+            torch.cuda.synchronize(dev)
+        kfac.overlap_invert = True
+        kfac.launch_first = 16
     if pre > 0:
         x = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
         t0 = time.perf_counter()
