@@ -241,10 +241,10 @@ class KFAC(Curvature):
         # frees them after each update): the queue is also launched once the records
         # it holds reach this many bytes, so a wide or conv model's activations are
         # not retained beyond ~this much (MLP batch of 4096: 17 MB per update; LeNet-5
-        # batch of 1024: ~35 MB; the wide MLP: 281 MB, one update per launch).  Round 5,
-        # same box: 512 MiB +4 % on LeNet-5 (14 updates per launch instead of 7), wide
-        # unchanged (still one per launch); 1 GiB +6 % on LeNet-5 but -1.6 % on the wide
-        # MLP (3-update launches)
+        # batch of 1024: ~35 MB; the wide MLP: 281 MB).  Round 5, same box: 512 MiB +4 %
+        # on LeNet-5 (9 launches per pass instead of 15), the wide MLP equal within 0.3 %
+        # (two updates per launch instead of one); 1 GiB +6 % on LeNet-5 but -1.6 % on
+        # the wide MLP (3-update launches)
         self.defer_bytes = 512 << 20
         self._queue_bytes = 0
         self._queue = []         # per queued update: (jobs, operand pointers, kept records,
@@ -827,7 +827,7 @@ class KFAC(Curvature):
         done.record(side_h)
         buf = self._acc_bufs[self._acc_par]
         self._acc_reads[buf.data_ptr()] = done
-        self._acc_par ^= 1
+        self._acc_par = (self._acc_par + 1) % len(self._acc_bufs)
 
     # ------------------------------------------------------------------ invert
     def _damping(self, add, multiply, count=None):

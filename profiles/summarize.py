@@ -58,15 +58,16 @@ def main(tag):
     if "FETCH_SIZE" in t and "WRITE_SIZE" in t:
         # FETCH_SIZE scale: x2 for 16 B/lane reads (MI355X_MICROARCH.md); the x3 kernel's
         # 4 B/lane buffer loads are calibrated by tools/fetch_calib.py (FETCH_X3_SCALE)
-        scale = FETCH_X3_SCALE if kname == "kfac_factor_tiles_x3" else 2.0
+        # (round 5: kfac_factor_syrk3 splits in the workgroup and reads fp32 rows by the
+        # same 4 B/lane buffer loads as the x3 kernel)
+        scale = FETCH_X3_SCALE if kname in ("kfac_factor_tiles_x3", "kfac_factor_syrk3") else 2.0
         fetch = t["FETCH_SIZE"]["mean_per_dispatch"] * 1024 * scale
         write = t["WRITE_SIZE"]["mean_per_dispatch"] * 1024
         note = (f"FETCH_SIZE x{scale:g} (gfx950 read-width correction) + WRITE_SIZE, KiB->bytes, "
                 "mean over the bench's launches (15 updates per pass, last batch short)")
         if kname == "kfac_factor_syrk3":
-            note += ("; kfac_factor_syrk3 reads the split pass's bf16x3 panel images "
-                     "(6 B per operand element) by global_load_lds_dwordx4 (16 B/lane: the x2 "
-                     "applies); the split pass (kfac_split3) is a separate launch")
+            note += ("; kfac_factor_syrk3 (round 5: split in the workgroup, no split pass) reads "
+                     "fp32 operand rows by buffer_load_dword (4 B/lane), scale as for the x3 kernel")
         if kname == "kfac_factor_tiles_x3":
             note += ("; kfac_factor_tiles_x3 reads fp32 operand rows by buffer_load_dword "
                      "(4 B/lane, 128 B per half-wave): scale calibrated on a 512 MB operand "
