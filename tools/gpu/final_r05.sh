@@ -2,7 +2,7 @@
 # forced through kfac_factor_syrk3, smoke, the bench as the driver runs it
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r05_end3
+O=gpurun_out/${TAG:-r05_end4}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
 tail -2 $O/gpu_tests.log
