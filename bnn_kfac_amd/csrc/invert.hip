@@ -36,6 +36,24 @@
 
 #include "kfac_common.h"
 
+// Phase timestamps of the critical workgroup of each merged step (timing builds only:
+// tools/build_ab.sh NAME -DKFAC_INV_STAMPS=1, read by tools/probe_inv_stamps.py)
+#ifndef KFAC_INV_STAMPS
+#define KFAC_INV_STAMPS 0
+#endif
+#if KFAC_INV_STAMPS
+__device__ unsigned long long g_inv_stamps[96][16];
+#define INV_STAMP(st, ph)                                                          \
+  do {                                                                             \
+    if (threadIdx.x == 0 && blockIdx.x == 0 && (st) >= -1 && (st) < 95)            \
+      ::g_inv_stamps[(st) + 1][(ph)] = __builtin_amdgcn_s_memrealtime();         \
+  } while (0)
+#else
+#define INV_STAMP(st, ph) \
+  do {                    \
+  } while (0)
+#endif
+
 namespace kfac {
 namespace t64 {  // 64x64 fp64 tiles: the two-launch path of large factors (> 1536)
 constexpr int NB = 64;
@@ -161,6 +179,14 @@ int kfac_release_graphs() {
   t32::release_graphs();
   return KFAC_OK;
 }
+
+#if KFAC_INV_STAMPS
+extern "C" __attribute__((visibility("default"))) int kfac_debug_inv_stamps(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_inv_stamps), (size_t)n * sizeof(unsigned long long)) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif
 
 extern "C" int kfac_damped_inv_chol(const float* F, int n, int64_t ldF, double sqrt_s, double sqrt_n,
                                     float* L, int64_t ldL, void* workspace, size_t workspace_bytes,
