@@ -153,7 +153,7 @@ class Curvature(ABC):
 _SLAB_BYTES = 64 * 64 * 4
 
 # stream priority of the inversion side streams (-1 high; 0 normal measured within the
-# box spread)
+# box spread in rounds 4 and 5)
 _INV_STREAM_PRIO = -1
 
 
