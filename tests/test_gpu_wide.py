@@ -62,3 +62,31 @@ def test_wide_eigvals_4097(wide_layer, hip_device):
     want = np.linalg.eigvalsh(A.astype(np.float64))
     assert ev.shape == (4097,) and np.all(np.diff(ev) >= 0)
     np.testing.assert_allclose(ev, want, rtol=1e-9, atol=1e-11 * np.abs(want).max())
+
+
+def test_wide_queued_pass_vs_fp64(hip_device):
+    """The C5 bench's launch shape: a Linear(4096, 4096) layer's updates QUEUED into one
+    multi-batch kfac_factor_syrk3 launch (launch_first 16, the 512 MiB records cap: two
+    4096-row batches per launch, as bench.py's wide pass runs them), then a shorter third
+    batch (the ragged-tail path: its own launch on top), deferred reduction -- against
+    the fp64 oracle's sum of per-batch means (curvatures.py:345-363), rtol 1e-5 of each
+    factor's scale."""
+    from bnn_kfac_amd.curvatures import KFAC
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(4096, 4096)).to(hip_device)
+    kfac = KFAC(net)
+    kfac.launch_first = 16
+    rng = np.random.default_rng(40961)
+    wantA = np.zeros((4097, 4097))
+    wantG = np.zeros((4096, 4096))
+    for rows in (4096, 4096, 1500):
+        a = rng.random((rows, 4096), dtype=np.float32)
+        g = rng.standard_normal((rows, 4096), dtype=np.float32)
+        kfac.record[net[0]] = [torch.from_numpy(a).to(hip_device), torch.from_numpy(g).to(hip_device)]
+        kfac.update(batch_size=rows)
+        wantA += O.linear_factor_A(a, True, np.float64)
+        wantG += O.grad_factor(g, np.float64)
+    A, G = (t.cpu().numpy() for t in kfac.state[net[0]])
+    for got, want in ((A, wantA), (G, wantG)):
+        np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-5 * np.abs(want).max())
+        assert np.array_equal(got, got.T)
