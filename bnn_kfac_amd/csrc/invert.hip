@@ -79,6 +79,7 @@ using namespace kfac;
 static bool small_tiles(const kfac_invert_job* jobs, int njobs) {
   const char* e = getenv("KFAC_INV_TILE");
   if (e && atoi(e) == 64) return false;
+  if (e && atoi(e) == 32) return true;  // (A/B: 32-tiles for every size)
   int m = 0;
   for (int i = 0; i < njobs; ++i) m = std::max(m, (int)jobs[i].n);
   return m <= 1536;
