@@ -129,6 +129,7 @@ SIGNATURES = {
     "kfac_invert_pipelined": (ctypes.c_int, [ctypes.POINTER(InvertJob), ctypes.c_int, c_vp, ctypes.c_size_t,
                                              c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "kfac_event_create": (ctypes.c_int, [ctypes.POINTER(c_vp)]),
+    "kfac_event_create_ex": (ctypes.c_int, [ctypes.POINTER(c_vp), ctypes.c_int]),
     "kfac_event_destroy": (ctypes.c_int, [c_vp]),
     "kfac_event_record": (ctypes.c_int, [c_vp, c_vp]),
     "kfac_stream_wait_event": (ctypes.c_int, [c_vp, c_vp]),
@@ -188,16 +189,21 @@ class RawEvent:
     cost the caller's thread 5-10 us per call.  Created on `device` (default: the
     current HIP device), like torch.cuda.Event on its stream's device; destroyed by
     close() or when the last reference goes (the KFAC event pools hold them)."""
-    __slots__ = ("handle",)
+    __slots__ = ("handle", "ordering")
 
-    def __init__(self, device=None):
+    def __init__(self, device=None, ordering=False):
+        """`ordering`: the event only orders one stream after another on the device
+        (kfac_event_create_ex flag 1: no system-scope fence); the host must not rely
+        on it to see device writes after synchronize()."""
         h = ctypes.c_void_p()
+        flags = 1 if ordering else 0
         if device is not None and torch.device(device).index is not None:
             with torch.cuda.device(device):
-                check(lib().kfac_event_create(ctypes.byref(h)), "kfac_event_create")
+                check(lib().kfac_event_create_ex(ctypes.byref(h), flags), "kfac_event_create_ex")
         else:
-            check(lib().kfac_event_create(ctypes.byref(h)), "kfac_event_create")
+            check(lib().kfac_event_create_ex(ctypes.byref(h), flags), "kfac_event_create_ex")
         self.handle = h.value
+        self.ordering = ordering
         _raw_events.add(self.handle)
 
     def close(self):

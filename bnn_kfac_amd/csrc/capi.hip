@@ -124,6 +124,16 @@ extern "C" int kfac_event_create(void** ev) {
              ? KFAC_OK
              : KFAC_ELAUNCH;
 }
+// flags bit 0: an ordering-only event (hipEventDisableSystemFence): no system-scope
+// release / acquire when it is recorded or waited on -- for events that only order one
+// stream after another on the same device; an event the host synchronizes with before
+// reading memory the device wrote keeps kfac_event_create's default
+extern "C" int kfac_event_create_ex(void** ev, int flags) {
+  if (!ev) return KFAC_EINVAL;
+  unsigned f = hipEventDisableTiming;
+  if (flags & 1) f |= hipEventDisableSystemFence;
+  return hipEventCreateWithFlags(reinterpret_cast<hipEvent_t*>(ev), f) == hipSuccess ? KFAC_OK : KFAC_ELAUNCH;
+}
 extern "C" int kfac_event_destroy(void* ev) {
   return hipEventDestroy((hipEvent_t)ev) == hipSuccess ? KFAC_OK : KFAC_ELAUNCH;
 }

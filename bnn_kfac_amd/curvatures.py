@@ -156,6 +156,11 @@ _SLAB_BYTES = 64 * 64 * 4
 # box spread in rounds 4 and 5)
 _INV_STREAM_PRIO = -1
 
+# stream-ordering events without the system-scope fence (KFAC._event): MLP line
+# 1.942-1.954e8 vs 1.912-1.940e8 img/s with every event fenced, 3 alternating reps,
+# LeNet-5 equal (profiles/r05bb/)
+_ORDERING_EVENTS = True
+
 
 # The inversion side streams, one pair per device for the whole process: a KFAC object
 # made after another (a new model, a new epoch's object) takes the same HIP streams.  New
@@ -892,7 +897,7 @@ class KFAC(Curvature):
                 pair.append(out)
             outs.append((layer, tuple(pair)))
         read = self._event(device) if side is not None else None
-        done, order = self._event(device), self._event(device)
+        done, order = self._event(device, ordering=False), self._event(device)
         host = self._pinned_host(len(jobs))
         after = main_h  # the stream the inversion is ordered after
         if side_reduce:
@@ -911,14 +916,18 @@ class KFAC(Curvature):
         if self.eager_verdict:
             self._check_inverse()
 
-    def _event(self, device):
+    def _event(self, device, ordering=True):
         """A raw HIP event (N.RawEvent) from the pool of settled ones (a verdict's `done`
-        after its host wait, an ordering event after the wait on it was enqueued)."""
-        pool = self._event_pool.get(device.index)
-        return pool.pop() if pool else N.RawEvent(device)
+        after its host wait, an ordering event after the wait on it was enqueued).
+        `ordering`: the event only orders streams on the device (no system-scope
+        fence); a verdict's `done`, which the host waits on before reading the pinned
+        copy, takes ordering=False."""
+        ordering = ordering and _ORDERING_EVENTS
+        pool = self._event_pool.get((device.index, ordering))
+        return pool.pop() if pool else N.RawEvent(device, ordering=ordering)
 
     def _pool_event(self, device, ev):
-        self._event_pool.setdefault(device.index, []).append(ev)
+        self._event_pool.setdefault((device.index, getattr(ev, "ordering", False)), []).append(ev)
 
     def _pinned_info(self, info):
         """A pinned host int32 buffer for a verdict readback (pooled)."""

@@ -352,6 +352,9 @@ KFAC_API int kfac_invert_pipelined(const kfac_invert_job* jobs, int njobs, void*
 /* Raw HIP events for the host side's stream ordering (no reference counterpart: the
  * reference is synchronous).  query: 1 complete, 0 pending, < 0 error. */
 KFAC_API int kfac_event_create(void** event);
+/* flags bit 0: ordering-only event (no system-scope fence when recorded / waited on):
+ * for stream-to-stream order on one device, not for host reads after a sync. */
+KFAC_API int kfac_event_create_ex(void** event, int flags);
 KFAC_API int kfac_event_destroy(void* event);
 KFAC_API int kfac_event_record(void* event, kfac_stream_t stream);
 KFAC_API int kfac_stream_wait_event(kfac_stream_t stream, void* event);

@@ -176,8 +176,9 @@ class _NoStream:
 
 class HostRawEvent:
     """Test double of N.RawEvent (host work is synchronous: always complete)."""
-    def __init__(self, device=None):
+    def __init__(self, device=None, ordering=False):
         self.handle = 0
+        self.ordering = ordering
 
     def close(self):
         pass
