@@ -2,6 +2,8 @@
 process, `reps` times each (200 steps, device sync around each block):
 
   full      bench.py's one_pass (reset, 15 updates, invert on the side stream)
+  sidereduce reset, 15 updates, the pass's reduce on the inversion's side stream with
+            invert()'s event order, no inversion
   noinv     reset, 15 updates, flush() (the pass's reduce on the caller's stream)
   launch    reset, 15 updates, the queue's launch only (x3 launches back to back)
   hostonly  reset, 15 updates with every device launch stubbed out (the host's own
@@ -55,6 +57,16 @@ def main():
         updates()
         kfac.flush()
 
+    def sidereduce():
+        # the pass's reduce on the side stream with invert()'s event order, no inversion
+        updates()
+        jobs = kfac._take_reduce()
+        if jobs:
+            dev_ = dev
+            main_h = N.stream_handle(dev_)
+            side = kfac._side_stream(dev_, alternate=True)
+            kfac._reduce_on_side(jobs, dev_, main_h, side.cuda_stream)
+
     def launch():
         updates()
         kfac._launch_queue()
@@ -69,7 +81,7 @@ def main():
         finally:
             N.factor_update = real_update
 
-    modes = {"full": full, "noinv": noinv, "launch": launch, "hostonly": hostonly}
+    modes = {"full": full, "sidereduce": sidereduce, "noinv": noinv, "launch": launch, "hostonly": hostonly}
     out = {m: [] for m in modes}
     for rep in range(reps):
         for name, fn in modes.items():
