@@ -727,8 +727,12 @@ def main(argv=None):
     # on (events recorded around each launch, on its stream).  Kept out of the timed
     # region above because the event packets add ~10 us per launch boundary.
     comm["timing"] = True
+    if world > 1:  # the side-stream collective (DistributedKFAC.side_collective) times itself
+        kfac.comm_events = comm.setdefault("events", [])
     prof = profiled_steps(N, one_pass, kfac, sync, args.steps)
     comm["timing"] = False
+    if world > 1:
+        kfac.comm_events = None
     allreduce_ms = None
     if world > 1:
         allreduce_ms = max_over_ranks(sum(a.elapsed_time(b) for a, b in comm.pop("events", []))

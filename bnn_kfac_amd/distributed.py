@@ -65,6 +65,14 @@ class DistributedKFAC(KFAC):
 
     `shard_inversion`: "auto" (shard when world > 1 and some factor is larger than
     1536), True or False.
+
+    Overlap (`side_collective`, default on): when `invert()` runs a pass's collective
+    and the inversion is replicated on a side stream (KFAC's latency-bound case), the
+    pass's reduce, the pack, the all-reduce and the unpack go to that side stream, in
+    front of the inversion, instead of the caller's stream: the next pass's SYRK
+    launches do not queue behind the collective.  A later `state` read on the caller's
+    stream is ordered after the unpack; the next pass's reduce into the same buffer is
+    ordered after the inversion has read it (KFAC._await_readers).
     """
 
     def __init__(self, model: Union[Module, Sequential], layer_types: Union[List[str], str] = None,
@@ -82,6 +90,12 @@ class DistributedKFAC(KFAC):
         self._global_buf, self._global_views = None, {}
         self._tri = {}             # name -> staging buffer of the packed-triangle collectives
         self._sharded_last = False
+        self.side_collective = True
+        self.comm_events = None    # a list: (start, end) timing events of side collectives
+        self._side_pass = False    # invert() is running the side-stream collective
+        self._side_local = None    # that pass's rank-local factors
+        self._coll_done = None     # event after the side stream's unpack (state readers wait)
+        self.side_collectives = 0  # passes whose collective ran on the side stream
 
     def _alpha(self, op) -> float:
         return 1.0 / (float(op.rows) * self._scale) if op.rows else float("inf")
@@ -109,6 +123,7 @@ class DistributedKFAC(KFAC):
         purely local, so `update(); kfac.state` holds the whole pass as with KFAC."""
         if getattr(self, "_pending", False) and not self._collective():
             self.allreduce()
+        self._await_collective()
         if getattr(self, "_pending", False):
             import warnings
             warnings.warn("DistributedKFAC.state read while this rank's pass is not all-reduced "
@@ -181,6 +196,23 @@ class DistributedKFAC(KFAC):
         return bool(self.shard_inversion)
 
     def invert(self, add=0., multiply=1.):
+        if self._side_ok():
+            # KFAC.invert with the hooks below: _take_reduce hands the pass's reduce
+            # over and points `state` at the reduced buffer, _reduce_on_side runs the
+            # reduce + collective on the side stream, _release defers the buffer guard
+            self._side_pass = True
+            try:
+                return super().invert(add, multiply)
+            except BaseException:
+                # raised after _take_reduce took the pass (e.g. the previous inversion's
+                # singular verdict, which every rank sees alike): KFAC.invert reduced it
+                # on the caller's stream; run its collective there too
+                if self._side_local is not None:
+                    self._collective_on_caller(self._side_local)
+                raise
+            finally:
+                self._side_pass = False
+                self._side_local = None
         self.allreduce()
         assert self.state, "State dict is empty. Did you call 'update' prior to this?"
         entries = list(self.state.items())
@@ -190,6 +222,109 @@ class DistributedKFAC(KFAC):
         self._invert_sharded(entries, add, multiply)
         if self.eager_verdict:
             self._check_inverse()
+
+    # ------------------------------------------- side-stream collective (invert)
+    def _side_ok(self):
+        """The pass's collective can run on the inversion's side stream: a pending pass
+        that needs one, the first pass since reset (state empty: the reduced buffer
+        becomes the state, no accumulate), CUDA factors, the replicated inversion."""
+        if not (self.side_collective and self._pending and self._collective() and self.overlap_invert):
+            return False
+        if self._state or not self._local_state or self._packed is None:
+            return False
+        factors = [F_ for v in self._local_state.values() for F_ in v]
+        if not all(F_.is_cuda for F_ in factors):
+            return False
+        if self._shard_now(list(self._local_state.items())):
+            return False
+        return all(F_.data_ptr() == v.data_ptr() for layer in self._local_state
+                   for F_, v in zip(self._local_state[layer], self._packed_views.get(layer, ())))
+
+    def _take_reduce(self):
+        if not self._side_pass:
+            return super()._take_reduce()
+        reduced = self._state
+        self._state = self._local_state
+        try:
+            jobs = super()._take_reduce()
+        finally:
+            self._state = reduced
+        if jobs is None:  # (not on the side stream after all: the usual path)
+            self._side_pass = False
+            self.allreduce()
+            return None
+        # the reduced buffer becomes the state (its contents arrive on the side stream
+        # before the inversion reads them); the next pass accumulates into a fresh one
+        local = self._local_state
+        self._side_local = local
+        self._state = {layer: list(v) for layer, v in local.items()}
+        self._local_state = {}
+        self._pending = False
+        return jobs
+
+    def _reduce_on_side(self, jobs, device, main_h, side_h):
+        # (the side stream first waits for the previous inversion's read of this buffer:
+        # KFAC._await_readers on self._packed, registered by _release below)
+        super()._reduce_on_side(jobs, device, main_h, side_h)
+        if not self._side_pass:
+            return
+        # the reduced buffer is the state now; the next reset hands it out again
+        self._global_buf, self._global_views = self._packed, self._packed_views
+        self._packed, self._packed_views = None, {}
+        local, self._side_local = self._side_local, None
+        side = self._torch_stream(device, side_h)
+        with torch.cuda.stream(side):
+            t0 = t1 = None
+            if self.comm_events is not None:
+                t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                t0.record()
+            factors = [F for pair in local.values() for F in pair]
+            tj, total = N.tri_jobs(factors)
+            buf = self._buffer(f"reduce_{side_h}", total, device)  # one per side stream
+            N.tri_pack(tj, buf)
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+            N.tri_unpack(tj, buf, N.TRI_SYMMETRIC)
+            if t1 is not None:
+                t1.record()
+                self.comm_events.append((t0, t1))
+        done = self._event(device)
+        done.record(side_h)
+        self._coll_done = (done, device)
+        self.side_collectives += 1
+
+    def _collective_on_caller(self, local):
+        factors = [F for pair in local.values() for F in pair]
+        tj, total = N.tri_jobs(factors)
+        buf = self._buffer("reduce", total, factors[0].device)
+        N.tri_pack(tj, buf)
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+        N.tri_unpack(tj, buf, N.TRI_SYMMETRIC)
+        self._global_buf, self._global_views = self._packed, self._packed_views
+        self._packed, self._packed_views = None, {}
+
+    def _release(self, main_h, read, entries, device):
+        if not self._side_pass:
+            return super()._release(main_h, read, entries, device)
+        # the caller's stream goes on; the buffer's next writer (the next pass's reduce
+        # once reset() hands it out again) waits for the inversion's read instead
+        self._buf_read[self._global_buf.data_ptr()] = read
+
+    def _await_collective(self, wait=True):
+        """Order the caller's stream after the side stream's unpack (a `state` read);
+        wait=False only returns the event to the pool (reset: the state is dropped)."""
+        if self._coll_done is not None:
+            ev, dev = self._coll_done
+            self._coll_done = None
+            if wait:
+                self._wait(ev, None, dev)
+            self._pool_event(dev, ev)
+
+    def _torch_stream(self, device, handle):
+        streams = self._inv_streams.get(device.index)
+        for st in (streams if isinstance(streams, list) else [streams]):
+            if st is not None and st.cuda_stream == handle:
+                return st
+        return torch.cuda.ExternalStream(handle, device=device)
 
     def _invert_sharded(self, entries, add, multiply):
         """Each rank inverts the factors it owns (one grouped kfac_invert on the
@@ -266,6 +401,7 @@ class DistributedKFAC(KFAC):
 
     def reset(self):
         """Start a new pass, recycling the buffer the previous pass reduced into."""
+        self._await_collective(wait=False)
         if self._global_buf is not None and self._packed is None:
             self._packed, self._packed_views = self._global_buf, self._global_views
             self._global_buf, self._global_views = None, {}

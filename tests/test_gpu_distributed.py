@@ -49,7 +49,7 @@ def _net(dev):
                                torch.nn.Linear(128, 10)).to(dev)
 
 
-def _worker(rank, world, port, q, shape, shard, backend, launch_first=1):
+def _worker(rank, world, port, q, shape, shard, backend, launch_first=1, side=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     # RCCL: one rank per GPU; gloo: every rank on device 0 (one-GPU boxes)
@@ -65,6 +65,7 @@ def _worker(rank, world, port, q, shape, shard, backend, launch_first=1):
         kfac = DistributedKFAC(net, shard_inversion=shard)
         kfac.always_reduce = True
         kfac.launch_first = launch_first  # (16: the bench's pipelined loop, a pass per launch)
+        kfac.side_collective = side  # the pass's collective on the inversion's side stream
         for p in range(SIZES[shape][1]):
             kfac.reset()
             for a1, g1, a2, g2 in _data(shape):
@@ -78,7 +79,7 @@ def _worker(rank, world, port, q, shape, shard, backend, launch_first=1):
             kfac.invert(0.04, 200)
         st = [t.cpu().numpy() for pair in kfac.state.values() for t in pair]
         inv = [t.cpu().numpy() for pair in kfac.inv_state.values() for t in pair]
-        q.put((rank, st, inv, kfac._sharded_last))
+        q.put((rank, st, inv, kfac._sharded_last, kfac.side_collectives))
     finally:
         dist.destroy_process_group()
 
@@ -96,11 +97,11 @@ def _single_device(dev, shape):
             [t.cpu().numpy() for pair in kfac.inv_state.values() for t in pair])
 
 
-def _run(world, shape, shard, backend="gloo", launch_first=1):
+def _run(world, shape, shard, backend="gloo", launch_first=1, side=True):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, shape, shard, backend, launch_first))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, shape, shard, backend, launch_first, side))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -111,9 +112,15 @@ def _run(world, shape, shard, backend="gloo", launch_first=1):
     return results
 
 
-def _check(results, want_st, want_inv, shard):
-    for rank, st, inv, sharded in results:
+def _check(results, want_st, want_inv, shard, side=True, expect_side=False):
+    for rank, st, inv, sharded, side_passes in results:
         assert sharded == bool(shard)
+        # the pass's collective ran on the inversion's side stream only when allowed
+        # (replicated inversion); in the bench's shape (one launch per pass) it did
+        if not side or shard:
+            assert side_passes == 0, side_passes
+        if expect_side:
+            assert side_passes > 0, side_passes
         for g, w in zip(st, want_st):
             np.testing.assert_allclose(g, w, rtol=1e-5, atol=1e-5 * np.abs(w).max())
         # the reduced factors differ from the single-device sums in the last bits,
@@ -126,12 +133,13 @@ def _check(results, want_st, want_inv, shard):
         np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("shape,shard,lf", [("small", False, 1), ("c4", False, 1), ("small", True, 1),
-                                            ("c4", False, 16)])
-def test_two_ranks_match_single_device(hip_device, shape, shard, lf):
-    results = _run(2, shape, shard, launch_first=lf)
+@pytest.mark.parametrize("shape,shard,lf,side", [("small", False, 1, True), ("c4", False, 1, True),
+                                                 ("small", True, 1, True), ("c4", False, 16, True),
+                                                 ("c4", False, 16, False)])
+def test_two_ranks_match_single_device(hip_device, shape, shard, lf, side):
+    results = _run(2, shape, shard, launch_first=lf, side=side)
     want_st, want_inv = _single_device(hip_device, shape)
-    _check(results, want_st, want_inv, shard)
+    _check(results, want_st, want_inv, shard, side, expect_side=side and lf == 16)
 
 
 @pytest.mark.parametrize("shard", [False, True])
@@ -151,7 +159,7 @@ def test_rccl_two_ranks_two_gpus(hip_device, shape, shard):
         pytest.skip("needs 2 GPUs (one RCCL rank per GPU)")
     results = _run(2, shape, shard, backend="nccl", launch_first=16)
     want_st, want_inv = _single_device(hip_device, shape)
-    _check(results, want_st, want_inv, shard)
+    _check(results, want_st, want_inv, shard, expect_side=not shard)
 
 
 def test_bench_two_ranks_parity_field(tmp_path):
