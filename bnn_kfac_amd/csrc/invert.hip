@@ -178,6 +178,8 @@ extern "C" int kfac_invert(const kfac_invert_job* jobs, int njobs, void* workspa
 int kfac_release_graphs() {
   t64::release_graphs();
   t32::release_graphs();
+  t64::release_look_ahead();
+  t32::release_look_ahead();
   return KFAC_OK;
 }
 

@@ -3,7 +3,7 @@ stream, overlap off), median over `reps` of torch.cuda events around each call, 
 factors of one bench pass.  The library is the in-tree one unless BNN_KFAC_AMD_LIB
 points elsewhere (same-box A/B of builds, one process each).
 
-    python tools/probe_invert.py [reps] [tag]
+    python tools/probe_invert.py [reps] [tag] [config]   (config: mlp, or wide for C5)
 """
 import json
 import sys
@@ -18,12 +18,13 @@ from bnn_kfac_amd.curvatures import KFAC  # noqa: E402
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     tag = sys.argv[2] if len(sys.argv) > 2 else ""
+    cfg = sys.argv[3] if len(sys.argv) > 3 else "mlp"
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     torch.cuda.set_stream(torch.cuda.Stream(dev))
-    specs = bench.CONFIGS["mlp"]
-    batch, images = bench.SHAPES[("mlp", 1)]
-    net = bench.build_model("mlp", dev)
+    specs = bench.CONFIGS[cfg]
+    batch, images = bench.SHAPES[(cfg, 1)]
+    net = bench.build_model(cfg, dev)
     layers = [m for m in net.modules() if isinstance(m, torch.nn.Linear)]
     recs = bench.synthetic_records(specs, images, dev, seed=1234)
     kfac = KFAC(net)
