@@ -142,13 +142,14 @@ def test_two_ranks_match_single_device(hip_device, shape, shard, lf, side):
     _check(results, want_st, want_inv, shard, side, expect_side=side and lf == 16)
 
 
-@pytest.mark.parametrize("shard", [False, True])
-def test_rccl_world1_collectives(hip_device, shard):
+@pytest.mark.parametrize("shard,lf", [(False, 1), (True, 1), (False, 16)])
+def test_rccl_world1_collectives(hip_device, shard, lf):
     """The RCCL (nccl backend) all-reduce of the packed triangles and, sharded, the
-    all-gather of the L factors, at world 1: results equal plain KFAC's."""
-    results = _run(1, "small", shard, backend="nccl")
+    all-gather of the L factors, at world 1: results equal plain KFAC's.  With one
+    launch per pass (lf 16) the all-reduce runs on the inversion's side stream."""
+    results = _run(1, "small", shard, backend="nccl", launch_first=lf)
     want_st, want_inv = _single_device(hip_device, "small")
-    _check(results, want_st, want_inv, shard)
+    _check(results, want_st, want_inv, shard, expect_side=lf == 16 and not shard)
 
 
 @pytest.mark.parametrize("shape,shard", [("small", False), ("c4", False), ("small", True)])
