@@ -237,8 +237,10 @@ class DistributedKFAC(KFAC):
             return False
         if self._shard_now(list(self._local_state.items())):
             return False
-        return all(F_.data_ptr() == v.data_ptr() for layer in self._local_state
-                   for F_, v in zip(self._local_state[layer], self._packed_views.get(layer, ())))
+        views = self._packed_views
+        return all(layer in views and len(views[layer]) == len(self._local_state[layer]) and
+                   all(F_.data_ptr() == v.data_ptr() for F_, v in zip(self._local_state[layer], views[layer]))
+                   for layer in self._local_state)
 
     def _take_reduce(self):
         if not self._side_pass:
