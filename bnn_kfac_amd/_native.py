@@ -23,7 +23,11 @@ ROWMAJOR, CHANNEL, PATCH = 0, 1, 2
 OUT_INV_CHOL, OUT_INVERSE = 0, 1
 TRI_SYMMETRIC, TRI_LOWER = 0, 1
 (PROF_FACTOR_TILES, PROF_FACTOR_REDUCE, PROF_INVERT, PROF_QUAD_TILES, PROF_FACTOR_SYRK3,
- PROF_FACTOR_X3) = 0, 1, 2, 3, 4, 5
+ PROF_FACTOR_X3, PROF_FACTOR_CONV, PROF_FACTOR_CHANNEL_SMALL, PROF_SYEV) = range(9)
+# profile slot -> the kernel family rocprofv3 names (kfac_prof_id, include/kfac_hip.h)
+PROF_FACTOR_KERNELS = {PROF_FACTOR_TILES: "kfac_factor_tiles_t", PROF_FACTOR_SYRK3: "kfac_factor_syrk3",
+                       PROF_FACTOR_X3: "kfac_factor_tiles_x3", PROF_FACTOR_CONV: "kfac_factor_conv",
+                       PROF_FACTOR_CHANNEL_SMALL: "kfac_factor_channel_small"}
 
 c_i32, c_i64, c_f32, c_f64, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_void_p
 
@@ -124,7 +128,11 @@ SIGNATURES = {
     "kfac_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "kfac_profile_read": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_int64)]),
+    "kfac_profile_read_work": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                              ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
     "kfac_profile_reset": (ctypes.c_int, []),
+    "kfac_set_knob": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
+    "kfac_get_knob": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     "kfac_release": (ctypes.c_int, []),
     "kfac_invert_pipelined": (ctypes.c_int, [ctypes.POINTER(InvertJob), ctypes.c_int, c_vp, ctypes.c_size_t,
                                              c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -590,3 +598,25 @@ def profile_read(kid: int):
     ms, n = ctypes.c_double(), ctypes.c_int64()
     check(lib().kfac_profile_read(kid, ctypes.byref(ms), ctypes.byref(n)), "kfac_profile_read")
     return ms.value, n.value
+
+
+def profile_read_work(kid: int):
+    """(total milliseconds, launches, algorithmic work) of slot `kid` since the last
+    reset; the work of a factor slot is the launches' flops sum K_rows * n (n + 1)."""
+    ms, n, w = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+    check(lib().kfac_profile_read_work(kid, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(w)),
+          "kfac_profile_read_work")
+    return ms.value, n.value, w.value
+
+
+# ------------------------------------------------------------------ knobs
+def set_knob(name: str, value: int):
+    """Change a per-call knob (KFAC_INV_GRAPH, KFAC_INV_LOOKAHEAD, KFAC_EIG_G, KFAC_EIG_RB)
+    between calls; the library reads its environment once, at load."""
+    check(lib().kfac_set_knob(name.encode(), int(value)), f"kfac_set_knob({name})")
+
+
+def get_knob(name: str) -> int:
+    v = ctypes.c_int()
+    check(lib().kfac_get_knob(name.encode(), ctypes.byref(v)), f"kfac_get_knob({name})")
+    return v.value

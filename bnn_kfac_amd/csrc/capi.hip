@@ -13,6 +13,71 @@ extern "C" const char* kfac_strerror(int status) {
 
 extern "C" const char* kfac_version(void) { return "bnn_kfac_amd 0.1.0 gfx950"; }
 
+// ------------------------------------------------------------------ knobs
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+
+#include "knobs.h"
+
+namespace kfac {
+namespace {
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+int env_mode(const char* name) {  // -1 auto, 0 off, 1 forced
+  const char* v = getenv(name);
+  return v && v[0] == '1' ? 1 : v && v[0] == '0' ? 0 : -1;
+}
+// read at library load (static initialisation of this object)
+Knobs g_knobs = [] {
+  Knobs k;
+  k.syrk3 = env_mode("KFAC_SYRK3");
+  k.tiles_x3 = env_mode("KFAC_TILES_X3");
+  k.conv_small = env_int("KFAC_CONV_SMALL", 1) != 0;
+  k.conv_k = std::max(0, env_int("KFAC_CONV_K", 0));
+  k.inv_graph = env_int("KFAC_INV_GRAPH", 1) != 0;
+  k.inv_lookahead = env_int("KFAC_INV_LOOKAHEAD", 1) != 0;
+  k.eig_g = std::max(0, env_int("KFAC_EIG_G", 0));
+  k.eig_rb = env_int("KFAC_EIG_RB", 4) == 8 ? 8 : 4;
+  return k;
+}();
+}  // namespace
+const Knobs& knobs() { return g_knobs; }
+}  // namespace kfac
+
+// The per-call knobs (KFAC_INV_GRAPH, KFAC_INV_LOOKAHEAD, KFAC_EIG_G, KFAC_EIG_RB) may be
+// changed between calls; the kernel-selection ones are fixed at load (KFAC_EINVAL).
+extern "C" int kfac_set_knob(const char* name, int value) {
+  if (!name) return KFAC_EINVAL;
+  kfac::Knobs& k = kfac::g_knobs;
+  if (!strcmp(name, "KFAC_INV_GRAPH")) k.inv_graph = value != 0;
+  else if (!strcmp(name, "KFAC_INV_LOOKAHEAD")) k.inv_lookahead = value != 0;
+  else if (!strcmp(name, "KFAC_EIG_G") && value >= 0) k.eig_g = value;
+  else if (!strcmp(name, "KFAC_EIG_RB") && (value == 4 || value == 8)) k.eig_rb = value;
+  else return KFAC_EINVAL;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  return KFAC_OK;
+}
+
+extern "C" int kfac_get_knob(const char* name, int* value) {
+  if (!name || !value) return KFAC_EINVAL;
+  const kfac::Knobs& k = kfac::g_knobs;
+  if (!strcmp(name, "KFAC_SYRK3")) *value = k.syrk3;
+  else if (!strcmp(name, "KFAC_TILES_X3")) *value = k.tiles_x3;
+  else if (!strcmp(name, "KFAC_CONV_SMALL")) *value = k.conv_small;
+  else if (!strcmp(name, "KFAC_CONV_K")) *value = k.conv_k;
+  else if (!strcmp(name, "KFAC_INV_GRAPH")) *value = k.inv_graph;
+  else if (!strcmp(name, "KFAC_INV_LOOKAHEAD")) *value = k.inv_lookahead;
+  else if (!strcmp(name, "KFAC_EIG_G")) *value = k.eig_g;
+  else if (!strcmp(name, "KFAC_EIG_RB")) *value = k.eig_rb;
+  else return KFAC_EINVAL;
+  return KFAC_OK;
+}
+
 // ------------------------------------------------------------------ profiling
 #include <mutex>
 #include <vector>
@@ -22,6 +87,7 @@ namespace {
 struct Rec {
   int id;
   hipEvent_t start, stop;
+  double work;  // algorithmic flops (or bytes) of the scope, 0 if none
 };
 std::mutex g_mu;
 bool g_on = false;
@@ -41,10 +107,15 @@ hipEvent_t take() {
 }
 }  // namespace
 
-void prof_begin(int id, hipStream_t s) {
+bool prof_on() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return g_on;
+}
+
+void prof_begin(int id, hipStream_t s, double work) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (!g_on) return;
-  Rec r{id, take(), take()};
+  Rec r{id, take(), take(), work};
   if (!r.start || !r.stop) return;
   (void)hipEventRecord(r.start, s);
   g_open.push_back(r);
@@ -72,9 +143,9 @@ extern "C" int kfac_profile_enable(int on) {
   return KFAC_OK;
 }
 
-extern "C" int kfac_profile_read(int id, double* total_ms, int64_t* launches) {
+extern "C" int kfac_profile_read_work(int id, double* total_ms, int64_t* launches, double* work) {
   std::lock_guard<std::mutex> lk(g_mu);
-  double tot = 0.0;
+  double tot = 0.0, wk = 0.0;
   int64_t cnt = 0;
   for (const Rec& r : g_done) {
     if (r.id != id) continue;
@@ -82,11 +153,17 @@ extern "C" int kfac_profile_read(int id, double* total_ms, int64_t* launches) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, r.start, r.stop) != hipSuccess) return KFAC_ELAUNCH;
     tot += ms;
+    wk += r.work;
     ++cnt;
   }
   if (total_ms) *total_ms = tot;
   if (launches) *launches = cnt;
+  if (work) *work = wk;
   return KFAC_OK;
+}
+
+extern "C" int kfac_profile_read(int id, double* total_ms, int64_t* launches) {
+  return kfac_profile_read_work(id, total_ms, launches, nullptr);
 }
 
 // Every HIP object the library keeps across calls -- the inversion's cached graphs,

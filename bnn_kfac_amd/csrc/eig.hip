@@ -253,7 +253,6 @@ struct TriArgs {
   double* e;           // n: off-diagonal of T (e[k] = T[k+1][k])
   double* U;           // n x n: row k = reflector u_k (entries k+1..n-1), or null
   double* tau;         // n: reflector scales (0: no reflection), or null
-  uint64_t* stamps;    // debug (KFAC_EIG_PROF): per step 5 s_memrealtime stamps of workgroup 0
 };
 
 // Wave sum in registers (no LDS crossbar): quad_perm xor 1 / xor 2 and row_ror 4 / 8
@@ -414,12 +413,6 @@ __global__ __launch_bounds__(NTHREADS) void eig_tridiag(TriArgs a) {
   if (wg == 0 && tid == 0) a.d[0] = x[0];
   double* up = vs[1];  // previous step's u (unused at k = 0)
 
-  auto stamp = [&](int k, int at) {
-    if (a.stamps && wg == 0 && tid == 0) {
-      a.stamps[(size_t)k * 5 + at] = __builtin_amdgcn_s_memrealtime();
-      if (at == 0) a.stamps[(size_t)8192 * 5 + k] = __builtin_amdgcn_s_memtime();
-    }
-  };
   __shared__ double rp[2][TB / 64][RB];  // per-wave partial dots of a row batch (batch parity)
   __shared__ double p1_s;
   __shared__ double red2[TB / 64];           // block_sum slot of the sigma reduction
@@ -427,7 +420,6 @@ __global__ __launch_bounds__(NTHREADS) void eig_tridiag(TriArgs a) {
       __builtin_amdgcn_make_buffer_rsrc(a.pub, 0, (int)(2 * 4 * (size_t)n * sizeof(gran_t)), 0x00020000);
   for (int k = 0; k + 2 < n; ++k) {
     const unsigned tag = (unsigned)k + 2u;
-    stamp(k, 0);
     gran_t* pub = a.pub + (size_t)(k & 1) * 4 * n;
     // 1. reflector (every workgroup, redundantly, same order -> same bits)
     const double alpha = x[k + 1];
@@ -448,7 +440,6 @@ __global__ __launch_bounds__(NTHREADS) void eig_tridiag(TriArgs a) {
     }
     if (a.U && wg == k % G)  // reflectors kept for the eigenvector back-transform
       for (int j = k + 1 + tid; j < n; j += TB) a.U[(size_t)k * n + j] = u_at(j);
-    stamp(k, 1);
 
     // 2. row pass, thread per column, RB owned rows at a time: the lazy rank-2
     //    update of step k-1, then a_i (column k+1) and p_i = tau A_k[i][k+1:] . u
@@ -508,7 +499,6 @@ __global__ __launch_bounds__(NTHREADS) void eig_tridiag(TriArgs a) {
         }
       }
     }
-    stamp(k, 2);
 
     // 3. exchange: every (p_j, a_j), j > k; c = sum p_j u_j from the gathered p
     //    (same tree in every workgroup), then w_j, x'_j.  Up to CH columns per
@@ -553,7 +543,6 @@ __global__ __launch_bounds__(NTHREADS) void eig_tridiag(TriArgs a) {
       }
     }
     const double c = block_sum1_w<W>(cs, red);  // (its barrier also publishes p1_s and fail_s)
-    stamp(k, 3);
     if (fail_s) return;
     const double K = 0.5 * tau * c;
     const double u1 = u0;
@@ -593,7 +582,6 @@ __global__ __launch_bounds__(NTHREADS) void eig_tridiag(TriArgs a) {
     // above; the sigma barrier publishes them (and separates this step's reads of
     // `red` / `red2` from the next step's writes of the other slot)
     sigma = block_sum1_w<W>(sig, red2);
-    stamp(k, 4);
     if (wg == 0 && tid == 0) a.d[k + 1] = xn[k + 1];
     up = x;
     x = xn;
@@ -861,10 +849,6 @@ struct TriPlan {
 };
 constexpr size_t TRI_LDS_BUDGET = 150 * 1024;
 
-static int eig_g_env() {
-  const char* v = getenv("KFAC_EIG_G");
-  return v ? atoi(v) : 0;
-}
 
 // the block zeroed before every launch: abort word, then the granules
 static size_t tri_zero_bytes(int n) {
@@ -888,14 +872,12 @@ static TriPlan tri_plan(int n, bool vecs) {
     // 5.1 / 4.8 / 4.8 / 5.2 / 5.2 us (fewer rows per workgroup shorten the row pass,
     // more workgroups lengthen the exchange)
     p.G = std::max(gmin, std::min(256, (n + 7) / 8));
-    const int env = eig_g_env();
-    if (env > 0) p.G = std::max(gmin, std::min(1024, env));
+    if (knobs().eig_g > 0) p.G = std::max(gmin, std::min(1024, knobs().eig_g));
   } else {
     p.G = 256;
   }
   p.R = (n + p.G - 1) / p.G;
-  const char* rb = getenv("KFAC_EIG_RB");
-  p.RB = rb && atoi(rb) == 8 ? 8 : 4;  // 4 rows per batch measured faster at every G tried
+  p.RB = knobs().eig_rb;  // 4 rows per batch (default) measured faster at every G tried
   p.shmem = vec + (p.lds_rows ? (size_t)p.R * row : 0);
   p.ws = tri_zero_bytes(n)                                       // abort + granules
          + 2 * align_up((size_t)n * sizeof(double), 256)         // d, e
@@ -944,38 +926,11 @@ static int tridiag_eig(const kfac_eig_job& j, char* ws, int32_t* info, hipStream
                                        : reinterpret_cast<const void*>(&eig_tridiag<false, 4>));
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.shmem) != hipSuccess)
     return KFAC_ELAUNCH;
-  static uint64_t* prof = nullptr;  // debug: step-phase stamps (KFAC_EIG_PROF=1; synchronises)
-  const bool want_prof = getenv("KFAC_EIG_PROF") != nullptr;
-  if (want_prof) {
-    if (!prof && hipMalloc(&prof, (size_t)8192 * 6 * sizeof(uint64_t)) != hipSuccess) return KFAC_ELAUNCH;
-    if (j.n > 8192) return KFAC_EINVAL;
-    t.stamps = prof;
-  }
   void* kargs[] = {&t};
   // cooperative: the runtime rejects a grid that cannot be co-resident (no deadlock)
   if (hipLaunchCooperativeKernel(fn, dim3(pl.G), dim3(NTHREADS), kargs, (unsigned)pl.shmem, stream) !=
       hipSuccess)
     return KFAC_ELAUNCH;
-  if (want_prof) {
-    std::vector<uint64_t> h((size_t)j.n * 5), clk((size_t)j.n);
-    if (hipMemcpyAsync(h.data(), prof, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, stream) != hipSuccess ||
-        hipMemcpyAsync(clk.data(), prof + (size_t)8192 * 5, clk.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
-                       stream) != hipSuccess ||
-        hipStreamSynchronize(stream) != hipSuccess)
-      return KFAC_ELAUNCH;
-    fprintf(stderr, "eig_tridiag shader clock %.0f MHz\n",
-            (double)(clk[(size_t)j.n - 3] - clk[0]) / (double)(h[(size_t)(j.n - 3) * 5] - h[0]) * 100.0);
-    double ph[5] = {0, 0, 0, 0, 0};
-    const int steps = j.n - 2;
-    for (int k = 0; k < steps; ++k) {
-      for (int q = 0; q < 4; ++q) ph[q] += (double)(h[(size_t)k * 5 + q + 1] - h[(size_t)k * 5 + q]);
-      if (k + 1 < steps) ph[4] += (double)(h[(size_t)(k + 1) * 5] - h[(size_t)k * 5 + 4]);
-    }
-    fprintf(stderr, "eig_tridiag n=%d G=%d R=%d: us/step reflector %.2f rowpass+publish %.2f "
-            "sweep1+c %.2f sweep2+x %.2f tail %.2f total %.2f ms\n", j.n, pl.G, pl.R,
-            ph[0] / steps / 100.0, ph[1] / steps / 100.0, ph[2] / steps / 100.0, ph[3] / steps / 100.0,
-            ph[4] / steps / 100.0, (double)(h[(size_t)(steps - 1) * 5 + 4] - h[0]) / 1e5);
-  }
   // one wave per eigenvalue; d and e^2 in LDS while 2 n doubles fit (n <= 9600), else
   // read from global memory
   const size_t bsh2 = (size_t)2 * j.n * sizeof(double);
@@ -1049,6 +1004,13 @@ extern "C" int kfac_syev(const kfac_eig_job* jobs, int njobs, void* workspace, s
   }
   if (workspace_bytes < kfac_eig_workspace_bytes(jobs, njobs)) return KFAC_EWORKSPACE;
   hipStream_t st = (hipStream_t)stream;
+  // profile slot with the tridiagonalisations' algorithmic bytes: each reflector reads
+  // and rewrites the trailing rows once, sum_k (n - k)^2 x 16 B ~ 16 n^3 / 3
+  double work = 0.0;
+  if (prof_on())
+    for (int i = 0; i < njobs; ++i)
+      if (jobs[i].n > EIG_LDS_MAX) work += 16.0 * (double)jobs[i].n * jobs[i].n * jobs[i].n / 3.0;
+  ProfScope ps(KFAC_PROF_SYEV, st, work);
   EigArgs args{};
   char* ws = (char*)workspace;
   auto flush = [&]() -> int {

@@ -839,24 +839,13 @@ constexpr int X3_THREADS = 128;
 // edge: the lower-triangle tiles, or with a thin last tile row (T >= 2 and at most 32
 // rows in it) the T-1 pairs (i, i) + (T-1, i), the other strictly lower tiles of rows
 // < T-1 and the corner (see X3_PAIR)
-static bool x3_pairing() {  // KFAC_X3_PAIR=0: no pairs (A/B)
-  static const bool on = [] {
-    const char* v = getenv("KFAC_X3_PAIR");
-    return v ? atoi(v) != 0 : true;
-  }();
-  return on;
-}
-static inline bool x3_thin(int n, int T) { return x3_pairing() && T >= 2 && n - TILE * (T - 1) <= 32; }
-// KFAC_X3_PAIR_XS=k: a thin-row x3 job with f full-tile K-splits gets S = f + f / k slabs
-// per tile, the last f / k of them written by extra K-splits of its pair units only
-// (0: none, the A/B)
-static int x3_pair_xs() {
-  static const int k = [] {
-    const char* v = getenv("KFAC_X3_PAIR_XS");
-    return v ? std::max(0, atoi(v)) : 5;
-  }();
-  return k;
-}
+static inline bool x3_thin(int n, int T) { return T >= 2 && n - TILE * (T - 1) <= 32; }
+// a thin-row x3 job with f full-tile K-splits gets S = f + f / k slabs per tile, the last
+// f / k of them written by extra K-splits of its pair units only; k = 5 (MNIST MLP, same
+// box, 200 steps: 3 / 5 / 10 / none 145.7 / 145.6 / 150.0 / 153.1 us per launch,
+// DESIGN.md 3.1c)
+constexpr int X3_PAIR_XS = 5;
+static inline int x3_pair_xs() { return X3_PAIR_XS; }
 // S / (k + 1) recovers f / k from S = f + f / k (f = k a + b, b <= k - 1)
 static inline int64_t x3_xsplits(int64_t S) { return x3_pair_xs() ? S / (x3_pair_xs() + 1) : 0; }
 __host__ __device__ inline int x3_units_of(int T, bool pair) { return T * (T + 1) / 2 - (pair ? T - 1 : 0); }
@@ -1794,13 +1783,7 @@ __global__ __launch_bounds__(NTHREADS) void kfac_factor_channel_small(FactorArgs
 }
 
 // KFAC_CONV_SMALL=0: channel factors with n <= 8 on the MFMA kernel (A/B checks)
-static bool conv_small_off() {
-  static const bool off = [] {
-    const char* v = getenv("KFAC_CONV_SMALL");
-    return v && v[0] == '0';
-  }();
-  return off;
-}
+static bool conv_small_off() { return !knobs().conv_small; }
 
 // Geometry of a conv job on the LDS-staged kernel; false: the job takes the
 // register-staged path (images too large, channel blocks not float4-shaped, or an
@@ -2026,6 +2009,11 @@ static int64_t job_stages(const kfac_factor_job& j) {
   if (job_ragged(j)) return job_sps(j) * (j.nseg - 1) + std::max<int64_t>(1, cdiv(j.x.last_rows, BK));
   return job_sps(j) * job_nseg(j);
 }
+// K rows of a job (every batch; conv operands: images x positions) -- the profile's work
+static int64_t job_krows(const kfac_factor_job& j) {
+  if (job_ragged(j)) return j.x.rows * (j.nseg - 1) + j.x.last_rows;
+  return j.x.rows * job_nseg(j);
+}
 
 // Split K so that the grouped launch fills the chip's workgroup slots (256 CUs x 4
 // resident workgroups) in as few dispatch rounds as possible with every task still
@@ -2055,13 +2043,7 @@ static bool job_glds(const kfac_factor_job& jb) {
 // MLP 4097^2 factors 1.17e6 vs 9.4e5 img/s; the MNIST MLP's n <= 785 8.1e7 vs 1.0e8
 // -- there the split pass's padded 6-byte images (785 -> 896, 129 -> 256 columns)
 // cost as much as the fp32 kernel's whole launch).  KFAC_SYRK3=1 / 0 forces it.
-static int syrk3_mode() {
-  static const int m = [] {
-    const char* v = getenv("KFAC_SYRK3");
-    return v && v[0] == '1' ? 1 : v && v[0] == '0' ? 0 : -1;
-  }();
-  return m;
-}
+static int syrk3_mode() { return knobs().syrk3; }
 
 // bytes of a job's pre-split panel images (kfac_factor_syrk3; narrow jobs: none)
 
@@ -2087,13 +2069,7 @@ static bool syrk3_group(const kfac_factor_job* jobs, int njobs) {
 // 0.61 ms (2 SYRK waves per SIMD instead of 4).  Groups whose largest factor has
 // n < 512 keep the fp32 kernel (LeNet-5's fully connected factors, n <= 401: 1.34e7
 // vs 1.39e7 img/s with x3).
-static int tiles_x3_mode() {
-  static const int m = [] {
-    const char* v = getenv("KFAC_TILES_X3");
-    return v && v[0] == '1' ? 1 : v && v[0] == '0' ? 0 : -1;
-  }();
-  return m;
-}
+static int tiles_x3_mode() { return knobs().tiles_x3; }
 
 static bool tiles_x3_group(const kfac_factor_job* jobs, int njobs) {
   if (tiles_x3_mode() == 0 || njobs <= 0 || syrk3_group(jobs, njobs)) return false;
@@ -2206,11 +2182,7 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
       // (mode-0 instances are compiled for KFAC_CONV_OCC resident workgroups per CU)
       const int64_t cslots = cg.mode == 0 ? (int64_t)KFAC_CONV_OCC * 256 : slots;
       int k = (int)std::max<int64_t>(1, cdiv((int64_t)cg.units * cg.B, small ? cslots / 2 : cslots));
-      static const int env_k = [] {
-        const char* v = getenv("KFAC_CONV_K");
-        return v ? atoi(v) : 0;
-      }();
-      if (env_k > 0) k = env_k;
+      if (knobs().conv_k > 0) k = knobs().conv_k;
       k = std::min(k, cg.B);
       p.splits = (int)cdiv(cg.B, k);
     }
@@ -2291,10 +2263,9 @@ static int prepare_group(const kfac_factor_job* jobs_in, int njobs, char* ws, si
   args = FactorArgs{};
   red = FactorArgs{};
   args.njobs = njobs;
-  {
-    const char* e = getenv("KFAC_SYRK_ORDER");
-    args.split_major = e ? atoi(e) : 1;
-  }
+  // split-major task order (each XCD a contiguous range of K-splits of all tiles):
+  // 55 k vs 194 k KiB fetched per launch tile-major at equal time
+  args.split_major = 1;
   int tasks = 0, rtiles = 0, nsegs = 0;
   size_t off = 0;
   for (int i = 0; i < njobs; ++i) {
@@ -2344,11 +2315,20 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
   const bool s3 = syrk3_group(jobs, njobs);
   const bool x3 = tiles_x3_group(jobs, njobs);
   {
-    ProfScope ps(s3 ? KFAC_PROF_FACTOR_SYRK3 : x3 ? KFAC_PROF_FACTOR_X3 : KFAC_PROF_FACTOR_TILES, stream);
     // launch_groups() gives every channel-major / im2col job a group of its own
     // conv jobs whose images fit LDS: the image-staged kernel
     ConvGeom cg;
     const bool staged = njobs == 1 && conv_geom(jobs[0], cg);
+    // one profile slot per kernel family (the name rocprofv3 reports), with the
+    // launch's algorithmic flops: sum over jobs of K rows x n (n + 1)
+    const int slot = s3 ? KFAC_PROF_FACTOR_SYRK3 : x3 ? KFAC_PROF_FACTOR_X3
+                     : !staged ? KFAC_PROF_FACTOR_TILES
+                     : (jobs[0].x.layout == KFAC_CHANNEL && cg.n <= 8 && !conv_small_off())
+                         ? KFAC_PROF_FACTOR_CHANNEL_SMALL : KFAC_PROF_FACTOR_CONV;
+    double work = 0.0;
+    if (prof_on())
+      for (int i = 0; i < njobs; ++i) work += (double)job_krows(jobs[i]) * factor_n(jobs[i]) * (factor_n(jobs[i]) + 1);
+    ProfScope ps(slot, stream, work);
     switch (jobs[0].x.layout) {
       case KFAC_CHANNEL:
         if (staged)

@@ -36,24 +36,6 @@
 
 #include "kfac_common.h"
 
-// Phase timestamps of the critical workgroup of each merged step (timing builds only:
-// tools/build_ab.sh NAME -DKFAC_INV_STAMPS=1, read by tools/probe_inv_stamps.py)
-#ifndef KFAC_INV_STAMPS
-#define KFAC_INV_STAMPS 0
-#endif
-#if KFAC_INV_STAMPS
-__device__ unsigned long long g_inv_stamps[96][16];
-#define INV_STAMP(st, ph)                                                          \
-  do {                                                                             \
-    if (threadIdx.x == 0 && blockIdx.x == 0 && (st) >= -1 && (st) < 95)            \
-      ::g_inv_stamps[(st) + 1][(ph)] = __builtin_amdgcn_s_memrealtime();         \
-  } while (0)
-#else
-#define INV_STAMP(st, ph) \
-  do {                    \
-  } while (0)
-#endif
-
 namespace kfac {
 namespace t64 {  // 64x64 fp64 tiles: the two-launch path of large factors (> 1536)
 constexpr int NB = 64;
@@ -75,11 +57,8 @@ using namespace kfac;
 // fits on a CU beside the 4 resident workgroups of a running SYRK launch, which leave
 // 32 KB: the inversion overlaps the next data pass instead of waiting for its
 // launches to drain); 64x64 tiles for larger factors (throughput-bound two-launch
-// steps).  KFAC_INV_TILE=64 forces 64 (A/B).
+// steps).
 static bool small_tiles(const kfac_invert_job* jobs, int njobs) {
-  const char* e = getenv("KFAC_INV_TILE");
-  if (e && atoi(e) == 64) return false;
-  if (e && atoi(e) == 32) return true;  // (A/B: 32-tiles for every size)
   int m = 0;
   for (int i = 0; i < njobs; ++i) m = std::max(m, (int)jobs[i].n);
   return m <= 1536;
@@ -183,13 +162,6 @@ int kfac_release_graphs() {
   return KFAC_OK;
 }
 
-#if KFAC_INV_STAMPS
-extern "C" __attribute__((visibility("default"))) int kfac_debug_inv_stamps(unsigned long long* out, int n) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_inv_stamps), (size_t)n * sizeof(unsigned long long)) == hipSuccess
-             ? 0
-             : -1;
-}
-#endif
 
 extern "C" int kfac_damped_inv_chol(const float* F, int n, int64_t ldF, double sqrt_s, double sqrt_n,
                                     float* L, int64_t ldL, void* workspace, size_t workspace_bytes,

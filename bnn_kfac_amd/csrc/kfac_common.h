@@ -10,6 +10,7 @@
 #include <stdint.h>
 
 #include "../../include/kfac_hip.h"
+#include "knobs.h"
 
 namespace kfac {
 
@@ -30,12 +31,16 @@ static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // ---- optional launch timing (capi.hip): Prof scope records hipEvents around a launch
-void prof_begin(int id, hipStream_t s);
+// `work`: the launch's algorithmic flops (factor kernels: sum over jobs of K rows x
+// n(n+1), the lower triangle incl. the diagonal at 2 flops per product), summed per
+// slot by kfac_profile_read_work so a roofline names its own kernel's work
+bool prof_on();
+void prof_begin(int id, hipStream_t s, double work = 0.0);
 void prof_end(int id, hipStream_t s);
 struct ProfScope {
   int id;
   hipStream_t s;
-  ProfScope(int id_, hipStream_t s_) : id(id_), s(s_) { prof_begin(id, s); }
+  ProfScope(int id_, hipStream_t s_, double work = 0.0) : id(id_), s(s_) { prof_begin(id, s, work); }
   ~ProfScope() { prof_end(id, s); }
 };
 

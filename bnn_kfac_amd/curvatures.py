@@ -855,6 +855,7 @@ class KFAC(Curvature):
         # the pass's deferred reduction: on the inversion's side stream (_take_reduce),
         # or completed here on the caller's stream by the `state` read
         side_reduce = self._take_reduce()
+        handed = False  # the side stream has taken the pass's reduce
         try:
             state = self._state if side_reduce else self.state
             assert state, "State dict is empty. Did you call 'update' prior to this?"
@@ -867,44 +868,48 @@ class KFAC(Curvature):
             for layer, (first, second) in entries:
                 N.require_device(first, "state", layer)
                 N.require_device(second, "state", layer)
+            device = entries[0][1][0].device
+            # The inversion runs on a high-priority side stream (overlap_invert): its
+            # critical path is a chain of single-workgroup tile factorisations, so the
+            # next data pass's SYRK launches fill the rest of the chip meanwhile.  The
+            # side stream starts after the work that produced `state`; the caller's
+            # stream waits only until the factors have been READ (kfac_invert_ex's
+            # inputs_read event, after the first launch), so it may overwrite them.
+            # Host side (round 4): one kfac_invert_pipelined call orders the side stream after
+            # the caller's, runs the inversion, copies the verdict to pinned memory and
+            # records `done`, on raw HIP events (N.RawEvent): ~10 torch.cuda stream / event
+            # calls of 5-10 us each are gone from the caller's thread.  The L factors are
+            # allocated on the caller's stream: every use or release of them is ordered after
+            # `done` (_order_after), so the allocator's stream order covers the side stream.
+            main_h = N.stream_handle(device)
+            latency_bound = max(F_.shape[0] for _, v in entries for F_ in v) <= 24 * 64
+            side = self._side_stream(device, alternate=latency_bound) if self.overlap_invert else None
+            side_h = side.cuda_stream if side is not None else main_h
+            outs, jobs = [], []
+            for (layer, value), (n, s) in zip(entries, damping):
+                pair = []
+                for F_ in value:
+                    out = torch.empty_like(F_, memory_format=torch.contiguous_format)
+                    jobs.append(N.invert_job(F_, out, s ** 0.5, n ** 0.5))
+                    pair.append(out)
+                outs.append((layer, tuple(pair)))
+            read = self._event(device) if side is not None else None
+            done, order = self._event(device, ordering=False), self._event(device)
+            host = self._pinned_host(len(jobs))
+            after = main_h  # the stream the inversion is ordered after
+            if side_reduce:
+                if side is None or not latency_bound:  # (cannot happen: _take_reduce checked)
+                    raise RuntimeError("KFAC.invert: side-stream reduce without a side stream")
+                self._reduce_on_side(side_reduce, device, main_h, side_h)
+                handed = True
+                after = side_h
         except BaseException:
-            if side_reduce:  # raised before the side stream took it: reduce here after all
+            # raised before the side stream took the reduce (validation, the previous
+            # inversion's verdict, an allocation or event failure): reduce on the
+            # caller's stream after all, so `state` never keeps unreduced factors
+            if side_reduce and not handed:
                 self._end_cycle(side_reduce)
             raise
-        device = entries[0][1][0].device
-        # The inversion runs on a high-priority side stream (overlap_invert): its
-        # critical path is a chain of single-workgroup tile factorisations, so the
-        # next data pass's SYRK launches fill the rest of the chip meanwhile.  The
-        # side stream starts after the work that produced `state`; the caller's
-        # stream waits only until the factors have been READ (kfac_invert_ex's
-        # inputs_read event, after the first launch), so it may overwrite them.
-        # Host side (round 4): one kfac_invert_pipelined call orders the side stream after
-        # the caller's, runs the inversion, copies the verdict to pinned memory and
-        # records `done`, on raw HIP events (N.RawEvent): ~10 torch.cuda stream / event
-        # calls of 5-10 us each are gone from the caller's thread.  The L factors are
-        # allocated on the caller's stream: every use or release of them is ordered after
-        # `done` (_order_after), so the allocator's stream order covers the side stream.
-        main_h = N.stream_handle(device)
-        latency_bound = max(F_.shape[0] for _, v in entries for F_ in v) <= 24 * 64
-        side = self._side_stream(device, alternate=latency_bound) if self.overlap_invert else None
-        side_h = side.cuda_stream if side is not None else main_h
-        outs, jobs = [], []
-        for (layer, value), (n, s) in zip(entries, damping):
-            pair = []
-            for F_ in value:
-                out = torch.empty_like(F_, memory_format=torch.contiguous_format)
-                jobs.append(N.invert_job(F_, out, s ** 0.5, n ** 0.5))
-                pair.append(out)
-            outs.append((layer, tuple(pair)))
-        read = self._event(device) if side is not None else None
-        done, order = self._event(device, ordering=False), self._event(device)
-        host = self._pinned_host(len(jobs))
-        after = main_h  # the stream the inversion is ordered after
-        if side_reduce:
-            if side is None or not latency_bound:  # (cannot happen: _take_reduce checked)
-                raise RuntimeError("KFAC.invert: side-stream reduce without a side stream")
-            self._reduce_on_side(side_reduce, device, main_h, side_h)
-            after = side_h
         N.invert_pipelined(jobs, device, host, order, read, done, after, side_h, side)
         self._pool_event(device, order)  # (the side stream's wait captured its record)
         if read is not None:

@@ -123,7 +123,9 @@ class DistributedKFAC(KFAC):
         purely local, so `update(); kfac.state` holds the whole pass as with KFAC."""
         if getattr(self, "_pending", False) and not self._collective():
             self.allreduce()
-        self._await_collective()
+        # (as KFAC.state: the caller's later work on the factors is ordered after the
+        # side stream's unpack into them and the inversion reading them)
+        self._await_state()
         if getattr(self, "_pending", False):
             import warnings
             warnings.warn("DistributedKFAC.state read while this rank's pass is not all-reduced "
@@ -160,6 +162,10 @@ class DistributedKFAC(KFAC):
         if not self._pending:
             return
         self.flush()  # the rank-local factors are complete only after the deferred reduce
+        # the reduced state may still be in flight on a side stream: a previous pass's
+        # side collective unpacks into it and its inversion reads it there; the in-place
+        # accumulation below runs on the caller's stream, so it waits for both first
+        self._await_state()
         local = self._local_state
         if self._collective() and local:
             factors = [F for pair in local.values() for F in pair]
@@ -310,6 +316,18 @@ class DistributedKFAC(KFAC):
         # the caller's stream goes on; the buffer's next writer (the next pass's reduce
         # once reset() hands it out again) waits for the inversion's read instead
         self._buf_read[self._global_buf.data_ptr()] = read
+
+    def _await_state(self):
+        """Order the caller's stream after everything a side-stream pass still does
+        with the reduced buffer: the unpack that writes it (`_coll_done`) and the
+        inversion that reads it (its inputs-read event, registered by _release)."""
+        self._await_collective()
+        buf = self._global_buf
+        if buf is not None and self._buf_read:
+            ev = self._buf_read.pop(buf.data_ptr(), None)
+            if ev is not None:
+                self._wait(ev, None, buf.device)
+                self._pool_event(buf.device, ev)
 
     def _await_collective(self, wait=True):
         """Order the caller's stream after the side stream's unpack (a `state` read);

@@ -325,17 +325,25 @@ KFAC_API int kfac_tri_unpack(const kfac_tri_job* jobs, int njobs, const float* p
 /* -------------------------------------------------------------- profiling
  * Optional HIP-event timing of the library's own launches, recorded on the
  * stream each kernel is launched on (off by default; not graph-capturable when
- * on).  Kernel ids: 0 factor tiles (fp32-MFMA SYRK), 1 factor reduce, 2 whole
- * invert call, 3 quadform tiles, 4 factor tiles by the split-pass bf16x3 SYRK
- * (launch groups whose largest factor has n >= 2048, or KFAC_SYRK3=1; the split
- * pass included), 5 factor tiles by the bf16x3 SYRK that splits fp32 panels in
- * registers (kfac_factor_tiles_x3).  kfac_profile_read syncs the recorded
- * events.                                                                    */
+ * on).  One slot per kernel family, named as rocprofv3 names the kernels:
+ *   0 kfac_factor_tiles_t (fp32-MFMA SYRK: row-major, LDS-DMA, register-staged conv),
+ *   1 kfac_factor_reduce, 2 the whole invert call, 3 kfac_quad tiles,
+ *   4 kfac_factor_syrk3 (bf16x3, split in the workgroup; largest n >= 2048),
+ *   5 kfac_factor_tiles_x3 (bf16x3, split in registers; largest n >= 512),
+ *   6 kfac_factor_conv (image-staged conv factors, both the im2col and the
+ *     channel-major operand), 7 kfac_factor_channel_small (channel factors n <= 8),
+ *   8 the whole kfac_syev call.
+ * kfac_profile_read syncs the recorded events.  kfac_profile_read_work also
+ * returns the slot's algorithmic work: for the factor slots (0, 4-7) the flops
+ * sum_jobs K_rows * n (n + 1) of the launches (lower triangle incl. the diagonal,
+ * 2 flops per product; curvatures.py:341-356), 0 for the others. */
 enum kfac_prof_id { KFAC_PROF_FACTOR_TILES = 0, KFAC_PROF_FACTOR_REDUCE = 1, KFAC_PROF_INVERT = 2,
                     KFAC_PROF_QUAD_TILES = 3, KFAC_PROF_FACTOR_SYRK3 = 4, KFAC_PROF_FACTOR_X3 = 5,
-                    KFAC_PROF_COUNT = 6 };
+                    KFAC_PROF_FACTOR_CONV = 6, KFAC_PROF_FACTOR_CHANNEL_SMALL = 7, KFAC_PROF_SYEV = 8,
+                    KFAC_PROF_COUNT = 9 };
 KFAC_API int kfac_profile_enable(int on);
 KFAC_API int kfac_profile_read(int id, double* total_ms, int64_t* launches);
+KFAC_API int kfac_profile_read_work(int id, double* total_ms, int64_t* launches, double* work);
 KFAC_API int kfac_profile_reset(void);
 
 /* ------------------------------------------------------------------- misc */
@@ -367,6 +375,13 @@ KFAC_API int kfac_event_synchronize(void* event);
  * it with atexit); later calls simply rebuild what they need.  No reference
  * counterpart (the reference keeps no device state). */
 KFAC_API int kfac_release(void);
+
+/* Environment knobs, read once when the library is loaded.  get: any
+ * knob's current value (KFAC_EINVAL for an unknown name).  set: only the per-call ones
+ * (KFAC_INV_GRAPH, KFAC_INV_LOOKAHEAD, KFAC_EIG_G, KFAC_EIG_RB), between calls; the
+ * kernel-selection knobs (KFAC_SYRK3, KFAC_TILES_X3, KFAC_CONV_*) are fixed at load. */
+KFAC_API int kfac_set_knob(const char* name, int value);
+KFAC_API int kfac_get_knob(const char* name, int* value);
 
 KFAC_API const char* kfac_strerror(int status);
 KFAC_API const char* kfac_version(void);

@@ -49,7 +49,7 @@ def _net(dev):
                                torch.nn.Linear(128, 10)).to(dev)
 
 
-def _worker(rank, world, port, q, shape, shard, backend, launch_first=1, side=True):
+def _worker(rank, world, port, q, shape, shard, backend, launch_first=1, side=True, accumulate=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     # RCCL: one rank per GPU; gloo: every rank on device 0 (one-GPU boxes)
@@ -66,8 +66,13 @@ def _worker(rank, world, port, q, shape, shard, backend, launch_first=1, side=Tr
         kfac.always_reduce = True
         kfac.launch_first = launch_first  # (16: the bench's pipelined loop, a pass per launch)
         kfac.side_collective = side  # the pass's collective on the inversion's side stream
-        for p in range(SIZES[shape][1]):
-            kfac.reset()
+        passes = 2 if accumulate else SIZES[shape][1]
+        for p in range(passes):
+            # accumulate: update, invert, update, invert with no reset() in between --
+            # the second pass adds into the reduced state a side-stream collective
+            # unpacked and an inversion read (the caller's stream must wait)
+            if p == 0 or not accumulate:
+                kfac.reset()
             for a1, g1, a2, g2 in _data(shape):
                 gb = a1.shape[0]
                 cut = [0, gb // 2 + (37 if shape == "small" else 0), gb][rank:rank + 2] if world == 2 \
@@ -84,24 +89,26 @@ def _worker(rank, world, port, q, shape, shard, backend, launch_first=1, side=Tr
         dist.destroy_process_group()
 
 
-def _single_device(dev, shape):
+def _single_device(dev, shape, passes=1):
     from bnn_kfac_amd.curvatures import KFAC
     net = _net(dev)
     kfac = KFAC(net)
-    for a1, g1, a2, g2 in _data(shape):
-        kfac.record[net[0]] = [torch.from_numpy(a1).to(dev), torch.from_numpy(g1).to(dev)]
-        kfac.record[net[2]] = [torch.from_numpy(a2).to(dev), torch.from_numpy(g2).to(dev)]
-        kfac.update(a1.shape[0])
+    for _ in range(passes):
+        for a1, g1, a2, g2 in _data(shape):
+            kfac.record[net[0]] = [torch.from_numpy(a1).to(dev), torch.from_numpy(g1).to(dev)]
+            kfac.record[net[2]] = [torch.from_numpy(a2).to(dev), torch.from_numpy(g2).to(dev)]
+            kfac.update(a1.shape[0])
     kfac.invert(0.04, 200)
     return ([t.cpu().numpy() for pair in kfac.state.values() for t in pair],
             [t.cpu().numpy() for pair in kfac.inv_state.values() for t in pair])
 
 
-def _run(world, shape, shard, backend="gloo", launch_first=1, side=True):
+def _run(world, shape, shard, backend="gloo", launch_first=1, side=True, accumulate=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, shape, shard, backend, launch_first, side))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, shape, shard, backend, launch_first, side,
+                                               accumulate))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -140,6 +147,16 @@ def test_two_ranks_match_single_device(hip_device, shape, shard, lf, side):
     results = _run(2, shape, shard, launch_first=lf, side=side)
     want_st, want_inv = _single_device(hip_device, shape)
     _check(results, want_st, want_inv, shard, side, expect_side=side and lf == 16)
+
+
+def test_two_ranks_accumulate_without_reset(hip_device):
+    """Two passes with no reset() in between (update, invert, update, invert), one
+    launch per pass: pass 1's collective runs on the inversion's side stream, pass 2
+    adds its all-reduced factors into that state on the caller's stream.  Equals one
+    device accumulating both passes."""
+    results = _run(2, "small", False, launch_first=16, accumulate=True)
+    want_st, want_inv = _single_device(hip_device, "small", passes=2)
+    _check(results, want_st, want_inv, False, expect_side=True)
 
 
 @pytest.mark.parametrize("shard,lf", [(False, 1), (True, 1), (False, 16)])

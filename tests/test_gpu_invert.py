@@ -284,3 +284,58 @@ def test_back_to_back_throughput_bound_inversions(hip_device):
     L = LA.double()
     err = (L.t() @ R @ L - torch.eye(A.shape[0], device=hip_device, dtype=torch.float64)).abs().max()
     assert err < 1e-3, float(err)
+
+
+@pytest.mark.parametrize("where", ["invert_job", "pinned"])
+def test_invert_failure_keeps_the_reduce(hip_device, monkeypatch, where):
+    """invert() hands the pass's deferred reduce to the side stream (_take_reduce); a
+    failure after that hand-over was prepared but before the side stream took it (an
+    invert_job / allocation error, models/curvatures.py:381-392's inputs) must still
+    reduce the pass on the caller's stream: `state` then equals the fp64 pass sum,
+    and a retried invert() gives the same L as an undisturbed run."""
+    from bnn_kfac_amd import curvatures as C
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Linear(784, 128), nn.ReLU(), nn.Linear(128, 10)).to(hip_device)
+    g = torch.Generator(device=hip_device).manual_seed(11)
+    batches = [(torch.rand(1024, 784, device=hip_device, generator=g),
+                torch.randn(1024, 128, device=hip_device, generator=g),
+                torch.rand(1024, 128, device=hip_device, generator=g),
+                torch.randn(1024, 10, device=hip_device, generator=g)) for _ in range(3)]
+
+    def run(fail):
+        kfac = C.KFAC(net)
+        kfac.eager_verdict = False
+        kfac.launch_first = 16  # one launch at the flush: the reduce goes to the side stream
+        kfac.reset()
+        for a1, g1, a2, g2 in batches:
+            kfac.record[net[0]] = [a1, g1]
+            kfac.record[net[2]] = [a2, g2]
+            kfac.update(a1.shape[0])
+        if fail:
+            with monkeypatch.context() as m:
+                def boom(*a, **k):
+                    raise RuntimeError("injected")
+                if where == "invert_job":
+                    m.setattr(C.N, "invert_job", boom)
+                else:
+                    m.setattr(kfac, "_pinned_host", boom)
+                with pytest.raises(RuntimeError, match="injected"):
+                    kfac.invert(0.04, 200)
+        st = [t.cpu().numpy() for pair in kfac.state.values() for t in pair]
+        kfac.invert(0.04, 200)
+        inv = [t.cpu().numpy() for pair in kfac.inv_state.values() for t in pair]
+        return st, inv
+
+    st_bad, inv_bad = run(True)
+    st_ok, inv_ok = run(False)
+    ref = O.OracleKFAC(np.float64)
+    for a1, g1, a2, g2 in batches:
+        ref.update_linear("l0", a1.cpu().numpy(), g1.cpu().numpy(), True)
+        ref.update_linear("l1", a2.cpu().numpy(), g2.cpu().numpy(), True)
+    want = [ref.state["l0"][0], ref.state["l0"][1], ref.state["l1"][0], ref.state["l1"][1]]
+    for got, w in zip(st_bad, want):
+        np.testing.assert_allclose(got, w, rtol=1e-5, atol=1e-5 * np.abs(w).max())
+    for a, b in zip(st_bad, st_ok):
+        np.testing.assert_array_equal(a, b)
+    for a, b in zip(inv_bad, inv_ok):
+        np.testing.assert_array_equal(a, b)

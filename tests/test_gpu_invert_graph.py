@@ -9,8 +9,6 @@ models/curvatures.py:381-396's L = cholesky(inverse(sqrt(s)F + sqrt(n)I)):
 * more distinct shapes than the cache holds (eviction waits for the last replay);
 * kfac_release() mid-process (every cached graph destroyed, later calls rebuild).
 """
-import os
-
 import numpy as np
 import pytest
 import torch
@@ -32,12 +30,13 @@ def _invert(factors, damping, dev):
 
 
 def _uncached(factors, damping, dev):
-    os.environ["KFAC_INV_GRAPH"] = "0"
+    from bnn_kfac_amd import _native as N
+    N.set_knob("KFAC_INV_GRAPH", 0)  # (the library reads its environment once, at load)
     try:
         outs, info = _invert(factors, damping, dev)
         torch.cuda.synchronize()
     finally:
-        os.environ.pop("KFAC_INV_GRAPH", None)
+        N.set_knob("KFAC_INV_GRAPH", 1)
     assert not info.any()
     return [o.cpu() for o in outs]
 

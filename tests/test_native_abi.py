@@ -83,3 +83,28 @@ def test_sample_struct_layout(tmp_path):
     # argument validation happens before any launch
     assert N.lib().kfac_sample(N.as_array(N.SampleJob, [N.SampleJob()]), 1, 0, None, 0,
                                None) == N.KFAC_EWORKSPACE
+
+
+def test_knobs_read_once_and_settable_per_call():
+    """The environment knobs are read once, at load (knobs.h): get_knob reports them,
+    set_knob changes only the per-call ones; the kernel-selection ones refuse."""
+    import subprocess
+    import sys
+    from bnn_kfac_amd import _native as N
+    assert N.get_knob("KFAC_INV_GRAPH") in (0, 1)
+    before = N.get_knob("KFAC_INV_LOOKAHEAD")
+    N.set_knob("KFAC_INV_LOOKAHEAD", 0)
+    assert N.get_knob("KFAC_INV_LOOKAHEAD") == 0
+    N.set_knob("KFAC_INV_LOOKAHEAD", before)
+    for name in ("KFAC_SYRK3", "KFAC_TILES_X3", "KFAC_CONV_K", "KFAC_NO_SUCH_KNOB"):
+        with pytest.raises(N.NativeError):
+            N.set_knob(name, 1)
+    with pytest.raises(N.NativeError):
+        N.get_knob("KFAC_INV_PRIO")  # an A/B knob of earlier rounds, gone
+    # a fresh process sees its environment at load
+    code = ("from bnn_kfac_amd import _native as N; "
+            "print(N.get_knob('KFAC_SYRK3'), N.get_knob('KFAC_EIG_RB'), N.get_knob('KFAC_CONV_K'))")
+    env = dict(os.environ, KFAC_SYRK3="1", KFAC_EIG_RB="8", KFAC_CONV_K="3")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True,
+                         env=env, cwd=ROOT).stdout.split()
+    assert out == ["1", "8", "3"]
