@@ -61,6 +61,7 @@ MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md, chi
 # split): its roofline is the dense bf16 MFMA peak / 6 in fp32-equivalent flops
 MFMA_BF16_PEAK_TFLOPS = 2500.0
 SYRK3_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / 6
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 DAMPING = (0.2 ** 2, 200)     # invert(std**2, N), classification_ll_block.py:72-73,106
 
 
@@ -318,11 +319,15 @@ def verify_parity(kfac, net, specs, recs, batch, images, world, rank, device, sy
     return detail
 
 
+# the factor-product kernel families (profile slots of the library, named as rocprofv3
+# names them) that compute each fp32 product as six bf16 MFMA products
+BF16X3_KERNELS = ("kfac_factor_tiles_x3", "kfac_factor_syrk3")
+
+
 def load_traffic(config):
-    """The committed PMC profile of `config`'s dominant factor kernel (profiles/
-    summarize.py): {kernel, tag, hbm_bytes_per_launch, ...}, or None."""
-    name = "factor_tiles_pmc.json" if config == "mlp" else f"factor_tiles_pmc_{config}.json"
-    path = os.path.join(ROOT, "profiles", name)
+    """The committed PMC profile of `config`'s single-GPU bench (profiles/summarize.py):
+    {"tag", "kernels": {family: {hbm_bytes_per_launch, rocprof_trace, ...}}}, or None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -330,8 +335,9 @@ def load_traffic(config):
 
 
 def profiled_steps(N, one_pass, kfac, sync, steps):
-    """`steps` more pipelined steps with the library's HIP-event timing on: {profile
-    slot: (ms, launches)} of the factor-product kernels, the reduce and the inversion."""
+    """`steps` more pipelined steps with the library's HIP-event timing on: {kernel
+    family: (ms, launches, algorithmic flops, algorithmic bytes)} of every factor-product
+    kernel family (one library profile slot each), plus the reduce and the inversion."""
     N.profile_reset()
     N.profile_enable(True)
     for _ in range(steps):
@@ -339,54 +345,55 @@ def profiled_steps(N, one_pass, kfac, sync, steps):
     kfac.inv_state
     sync()
     N.profile_enable(False)
-    out = {name: N.profile_read(pid) for name, pid in
-           (("kfac_factor_tiles", N.PROF_FACTOR_TILES), ("kfac_factor_syrk3", N.PROF_FACTOR_SYRK3),
-            ("kfac_factor_tiles_x3", N.PROF_FACTOR_X3), ("reduce", N.PROF_FACTOR_REDUCE),
-            ("invert", N.PROF_INVERT))}
+    out = {name: N.profile_read_work(pid) for pid, name in N.PROF_FACTOR_KERNELS.items()}
+    out["reduce"] = N.profile_read(N.PROF_FACTOR_REDUCE)
+    out["invert"] = N.profile_read(N.PROF_INVERT)
     N.profile_reset()
     return out
 
 
 def roofline_of(prof, specs, images, steps, config):
-    """The roofline object of the dominant factor-product kernel (the one that took the
-    most time: kfac_factor_tiles / _x3, fp32 or bf16x3 MFMA, or kfac_factor_syrk3) and
-    the per-step kernel breakdown, from profiled_steps' timings of `steps` passes of
-    `images` images: achieved = algorithmic flops / the kernel's launch time."""
-    prods = {k: prof[k] for k in ("kfac_factor_tiles", "kfac_factor_syrk3", "kfac_factor_tiles_x3")}
-    prod_kernel = max(prods, key=lambda k: prods[k][0])
-    tiles_ms, tiles_n = prods[prod_kernel]
-    prods_ms = sum(v[0] for v in prods.values())
-    syrk3 = prod_kernel != "kfac_factor_tiles"
-    fpi = flops_per_image(specs)
-    flops_timed = fpi * images * steps
-    achieved = flops_timed / (tiles_ms * 1e-3) / 1e12 if tiles_ms > 0 else None
-    peak = SYRK3_PEAK_TFLOPS if syrk3 else MFMA_F32_PEAK_TFLOPS
-    # traffic: HBM bytes per launch of the same kernel from the committed rocprofv3 PMC
-    # passes of this config's single-GPU bench launch (null when the profile is of
-    # another kernel)
+    """The roofline object of the dominant factor-product kernel family (the one that
+    took the most time among the library's per-family profile slots) and the per-step
+    breakdown, from profiled_steps' timings of `steps` passes of `images` images.
+    achieved = that family's OWN algorithmic flops (the library sums K_rows * n (n + 1)
+    over the jobs it launched) / its launch time; traffic = the committed rocprofv3
+    PMC passes of the same family in this config's bench (profiles/pmc_<config>.json)."""
+    fams = {k: v for k, v in prof.items() if k not in ("reduce", "invert")}
+    kern = max(fams, key=lambda k: fams[k][0])
+    ms, launches, flops, abytes = fams[kern]
+    bf16x3 = kern in BF16X3_KERNELS
+    achieved = flops / (ms * 1e-3) / 1e12 if ms > 0 else None
+    peak = SYRK3_PEAK_TFLOPS if bf16x3 else MFMA_F32_PEAK_TFLOPS
     pmc = load_traffic(config)
-    pmc_ok = pmc is not None and pmc.get("kernel") == prod_kernel
+    k_pmc = (pmc or {}).get("kernels", {}).get(kern)
+    traffic = k_pmc.get("hbm_bytes_per_launch") if k_pmc else None
     roofline = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                 "frac": (achieved / peak) if achieved else None,
-                "traffic": pmc.get("hbm_bytes_per_launch") if pmc_ok else None,
-                "traffic_source": (f"profiles/{pmc.get('tag')}/: rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
-                                   f"mean per {prod_kernel} launch of the single-GPU {config} bench")
-                                  if pmc_ok else None,
-                "kernel": prod_kernel,
+                "traffic": traffic,
+                "traffic_source": (f"profiles/{pmc.get('tag')}/: rocprofv3 --pmc FETCH_SIZE x{k_pmc.get('fetch_scale', 2):g}"
+                                   f" + WRITE_SIZE, mean per {kern} launch of the single-GPU {config} bench "
+                                   f"(rocprofv3 kernel trace of that run: {k_pmc.get('rocprof_trace')})")
+                                  if k_pmc else None,
+                "kernel": kern,
                 # (the same rate against the fp32 MFMA peak, the basis of earlier rounds)
                 "frac_fp32_peak_basis": (achieved / MFMA_F32_PEAK_TFLOPS) if achieved else None,
                 "peak_basis": ("dense bf16 MFMA 2.5 PF / 6 products per fp32 product (fp32-equivalent)"
-                               if syrk3 else "dense fp32 MFMA"),
-                "launches": tiles_n,
-                "avg_launch_us": 1e3 * tiles_ms / max(tiles_n, 1),
-                # a launch covers every queued update of the pass (multi-batch jobs):
-                # per-launch figures are the step's algorithmic totals / its launches
-                "flops_per_launch": flops_timed / max(tiles_n, 1),
-                "algorithmic_bytes_per_launch": bytes_per_image(specs) * images * steps
-                                                / max(tiles_n, 1)}
-    breakdown = {"factor_tiles_ms_per_step": prods_ms / steps,
+                               if bf16x3 else "dense fp32 MFMA"),
+                "launches": launches,
+                "avg_launch_us": 1e3 * ms / max(launches, 1),
+                # the family's own work per launch (library profile slot), not the step's
+                "flops_per_launch": flops / max(launches, 1),
+                "algorithmic_bytes_per_launch": abytes / max(launches, 1)}
+    fam_rows = {k: {"ms_per_step": v[0] / steps, "launches_per_step": v[1] / steps,
+                    "tflops": (v[2] / (v[0] * 1e-3) / 1e12) if v[0] > 0 else None}
+                for k, v in fams.items() if v[1]}
+    breakdown = {"factor_tiles_ms_per_step": sum(v[0] for v in fams.values()) / steps,
+                 "factor_kernels": fam_rows,
                  "factor_reduce_ms_per_step": prof["reduce"][0] / steps,
-                 "invert_ms_per_step": prof["invert"][0] / steps}
+                 "invert_ms_per_step": prof["invert"][0] / steps,
+                 "factor_flops_per_step_check": sum(v[2] for v in fams.values()) / steps,
+                 "factor_flops_per_step_algorithmic": flops_per_image(specs) * images}
     return roofline, breakdown
 
 
@@ -438,10 +445,83 @@ def other_config(config, device, steps, warmup):
     del kfac, recs, views
     torch.cuda.empty_cache()
     return {"value": images * steps / elapsed, "unit": "images/s", "ms_per_step": 1e3 * elapsed / steps,
-            "steps": steps, "warmup": warmup,
+            "steps": steps, "warmup": warmup, "config": config, "batch": batch, "images": images,
             "workload": f"{BASELINE_CONFIG[(config, 1)]}: {NAMES[config]} KFAC factor pass over {images} "
                         f"images (batch {batch}) + invert{DAMPING}, pipelined as the headline",
             "roofline": roofline, "breakdown": breakdown}
+
+
+EIG_SIZES = (785, 4097)  # the MNIST MLP's layer-1 A factor; the wide MLP's (C5) 4096 + ones
+
+
+def eig_factor(n, seed=0):
+    """A synthetic SPD factor of size n: X X^T / n + 1e-3 I, X ~ N(0, 1) (fp32), the shape
+    of a KFAC A factor (a Wishart spectrum)."""
+    rng = np.random.default_rng(seed + n)
+    X = rng.standard_normal((n, n)).astype(np.float32)
+    return torch.from_numpy(X @ X.T / n + 1e-3 * np.eye(n, dtype=np.float32))
+
+
+def eig_leg(device, sizes=EIG_SIZES, reps=3):
+    """BASELINE C5's "HBM-bound eig reported" (models/utilities.py:120-141, get_eigenvalues:
+    symeig of every factor): the device eigenvalue path (kfac_syev: tridiagonalisation +
+    Sturm multisection, fp64) on one factor per size, timed by the library's HIP events
+    on its stream (profile slot KFAC_PROF_SYEV).  `achieved` = the tridiagonalisation's
+    algorithmic bytes (each reflector reads and rewrites the trailing rows once,
+    sum_k (n - k)^2 x 16 B ~ 16 n^3 / 3) / the call's time.  At n = 785 the rows stay in
+    LDS (latency-bound: one grid-wide exchange per reflector); at 4097 they stream from
+    HBM."""
+    from bnn_kfac_amd import _native as N
+    from bnn_kfac_amd.utilities import symeig
+    out = {}
+    for n in sizes:
+        F = eig_factor(n).to(device)
+        symeig([F])  # warm-up (also builds nothing: no caches on this path)
+        torch.cuda.synchronize(device)
+        N.profile_reset()
+        N.profile_enable(True)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ev = symeig([F])[0][0]
+        torch.cuda.synchronize(device)
+        wall = (time.perf_counter() - t0) / reps
+        N.profile_enable(False)
+        ms, calls, _, abytes = N.profile_read_work(N.PROF_SYEV)
+        N.profile_reset()
+        ms_call = ms / max(calls, 1)
+        gbs = abytes / max(calls, 1) / (ms_call * 1e-3) / 1e9 if ms_call > 0 else None
+        out[str(n)] = {"ms": ms_call, "wall_ms": 1e3 * wall, "calls": calls,
+                       "algorithmic_bytes": abytes / max(calls, 1),
+                       "roofline": {"bound": "hbm" if n > 2000 else "latency", "achieved": gbs,
+                                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": gbs / HBM_PEAK_GBS if gbs else None, "traffic": None,
+                                    "kernel": "eig_tridiag (+ eig_bisect)"},
+                       "eigvals_checksum": float(ev.sum())}
+        del F
+    torch.cuda.empty_cache()
+    return out
+
+
+def eig_cpu_baseline(sizes=EIG_SIZES, threads=None, budget_s=6.0):
+    """The reference's eigenvalue path on the host cores: torch.symeig's successor
+    torch.linalg.eigvalsh (LAPACK syevd) on the same fp32 factors (utilities.py:136-137
+    calls symeig on the fp32 KFAC factors), repeated within ~budget_s per size."""
+    if threads:
+        torch.set_num_threads(threads)
+    out = {}
+    for n in sizes:
+        F = eig_factor(n)
+        torch.linalg.eigvalsh(F)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            torch.linalg.eigvalsh(F)
+            reps += 1
+            if time.perf_counter() - t0 >= budget_s / len(sizes) or reps >= 50:
+                break
+        out[str(n)] = {"ms": 1e3 * (time.perf_counter() - t0) / reps, "reps": reps}
+    return {"value": out, "unit": "ms per eigenvalue solve", "cores": torch.get_num_threads(),
+            "kind": "port", "sample": f"torch {torch.__version__} CPU linalg.eigvalsh (LAPACK syevd) on the "
+                                      f"fp32 factor, fp32 as the reference's symeig, per size"}
 
 
 # ------------------------------------------------------------------ launcher
@@ -515,7 +595,9 @@ def main(argv=None):
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-serial", action="store_true")
     ap.add_argument("--no-other-configs", action="store_true",
-                    help="N = 1 MLP: skip the GPU-only C3 (LeNet-5) and C5 (wide MLP) lines")
+                    help="N = 1 MLP: skip the C3 (LeNet-5) and C5 (wide MLP) lines")
+    ap.add_argument("--no-eig", action="store_true",
+                    help="N = 1 MLP: skip the eigensolver leg (n = 785, 4097)")
     ap.add_argument("--launch-first", type=int, default=None,
                     help="queued updates in a pass's first SYRK launch (KFAC.launch_first) for both "
                          "loops (default: 16 for the pipelined loop, the library's 1 for the serial one)")
@@ -582,6 +664,9 @@ def main(argv=None):
         others = {"C5": other_config("wide", device, steps=10, warmup=2),
                   "C3": other_config("lenet", device, steps=20, warmup=2)}
         torch.cuda.empty_cache()
+    eig = None
+    if world == 1 and args.config == "mlp" and not args.no_eig and not args.strong:
+        eig = eig_leg(device)
 
     specs = CONFIGS[args.config]
     net = build_model(args.config, device)
@@ -804,6 +889,18 @@ def main(argv=None):
             ve, _, samplee = cpu_e2e_baseline(args.config, 60000, 256, threads=cores)
             cpu.update({"c1_batch256_value": vc1, "c1_batch256_sample": samplec1,
                         "e2e_value": ve, "e2e_sample": samplee})
+        # the other configs' CPU baselines: the same op sequence on a bounded sample of
+        # their workload, at the thread count the headline's baseline found best
+        for name, oc in (others or {}).items():
+            v_o, c_o, s_o = cpu_baseline(CONFIGS[oc["config"]], oc["images"], oc["batch"], budget_s=6.0,
+                                         threads=cores)
+            oc["cpu_baseline"] = {"value": v_o, "unit": "images/s", "cores": c_o, "kind": "port", "sample": s_o}
+        if eig is not None:
+            eig_cpu = eig_cpu_baseline(threads=cores)
+            for n, e in eig.items():
+                e["cpu_baseline_ms"] = eig_cpu["value"][n]["ms"]
+            eig_cpu["value"] = {n: v["ms"] for n, v in eig_cpu["value"].items()}
+            eig["cpu_baseline"] = eig_cpu
 
     if rank == 0:
         cfg = BASELINE_CONFIG[shape_key]
@@ -833,7 +930,9 @@ def main(argv=None):
                "parity": None if parity is None else parity["ok"], "parity_detail": parity,
                "serial_images_per_s": serial, "e2e_images_per_s": e2e,
                # BASELINE C3 / C5 on this GPU, same loop (GPU-only; N = 1 MLP runs)
-               "other_configs": others}
+               "other_configs": others,
+               # BASELINE C5's eig leg: kfac_syev values at the MLP's 785 and the wide 4097
+               "eig": eig}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -24,8 +24,9 @@ OUT_INV_CHOL, OUT_INVERSE = 0, 1
 TRI_SYMMETRIC, TRI_LOWER = 0, 1
 (PROF_FACTOR_TILES, PROF_FACTOR_REDUCE, PROF_INVERT, PROF_QUAD_TILES, PROF_FACTOR_SYRK3,
  PROF_FACTOR_X3, PROF_FACTOR_CONV, PROF_FACTOR_CHANNEL_SMALL, PROF_SYEV) = range(9)
-# profile slot -> the kernel family rocprofv3 names (kfac_prof_id, include/kfac_hip.h)
-PROF_FACTOR_KERNELS = {PROF_FACTOR_TILES: "kfac_factor_tiles_t", PROF_FACTOR_SYRK3: "kfac_factor_syrk3",
+# profile slot -> the kernel family rocprofv3 names (kfac_prof_id, include/kfac_hip.h; the
+# fp32 SYRK is the template kfac_factor_tiles_t<...>, named without the _t as in profiles/)
+PROF_FACTOR_KERNELS = {PROF_FACTOR_TILES: "kfac_factor_tiles", PROF_FACTOR_SYRK3: "kfac_factor_syrk3",
                        PROF_FACTOR_X3: "kfac_factor_tiles_x3", PROF_FACTOR_CONV: "kfac_factor_conv",
                        PROF_FACTOR_CHANNEL_SMALL: "kfac_factor_channel_small"}
 
@@ -129,7 +130,8 @@ SIGNATURES = {
     "kfac_profile_read": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_int64)]),
     "kfac_profile_read_work": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
-                                              ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
+                                              ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double),
+                                              ctypes.POINTER(ctypes.c_double)]),
     "kfac_profile_reset": (ctypes.c_int, []),
     "kfac_set_knob": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
     "kfac_get_knob": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
@@ -601,12 +603,14 @@ def profile_read(kid: int):
 
 
 def profile_read_work(kid: int):
-    """(total milliseconds, launches, algorithmic work) of slot `kid` since the last
-    reset; the work of a factor slot is the launches' flops sum K_rows * n (n + 1)."""
-    ms, n, w = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
-    check(lib().kfac_profile_read_work(kid, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(w)),
+    """(total milliseconds, launches, algorithmic flops, algorithmic bytes) of slot `kid`
+    since the last reset (kfac_profile_read_work: a factor slot's flops are sum K_rows *
+    n (n + 1), its bytes every operand read once)."""
+    ms, n = ctypes.c_double(), ctypes.c_int64()
+    w, b = ctypes.c_double(), ctypes.c_double()
+    check(lib().kfac_profile_read_work(kid, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(w), ctypes.byref(b)),
           "kfac_profile_read_work")
-    return ms.value, n.value, w.value
+    return ms.value, n.value, w.value, b.value
 
 
 # ------------------------------------------------------------------ knobs

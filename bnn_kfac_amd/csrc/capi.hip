@@ -87,7 +87,8 @@ namespace {
 struct Rec {
   int id;
   hipEvent_t start, stop;
-  double work;  // algorithmic flops (or bytes) of the scope, 0 if none
+  double work;   // algorithmic flops of the scope, 0 if none
+  double bytes;  // algorithmic HBM bytes of the scope, 0 if none
 };
 std::mutex g_mu;
 bool g_on = false;
@@ -112,10 +113,10 @@ bool prof_on() {
   return g_on;
 }
 
-void prof_begin(int id, hipStream_t s, double work) {
+void prof_begin(int id, hipStream_t s, double work, double bytes) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (!g_on) return;
-  Rec r{id, take(), take(), work};
+  Rec r{id, take(), take(), work, bytes};
   if (!r.start || !r.stop) return;
   (void)hipEventRecord(r.start, s);
   g_open.push_back(r);
@@ -143,9 +144,10 @@ extern "C" int kfac_profile_enable(int on) {
   return KFAC_OK;
 }
 
-extern "C" int kfac_profile_read_work(int id, double* total_ms, int64_t* launches, double* work) {
+extern "C" int kfac_profile_read_work(int id, double* total_ms, int64_t* launches, double* work,
+                                      double* bytes) {
   std::lock_guard<std::mutex> lk(g_mu);
-  double tot = 0.0, wk = 0.0;
+  double tot = 0.0, wk = 0.0, by = 0.0;
   int64_t cnt = 0;
   for (const Rec& r : g_done) {
     if (r.id != id) continue;
@@ -154,16 +156,18 @@ extern "C" int kfac_profile_read_work(int id, double* total_ms, int64_t* launche
     if (hipEventElapsedTime(&ms, r.start, r.stop) != hipSuccess) return KFAC_ELAUNCH;
     tot += ms;
     wk += r.work;
+    by += r.bytes;
     ++cnt;
   }
   if (total_ms) *total_ms = tot;
   if (launches) *launches = cnt;
   if (work) *work = wk;
+  if (bytes) *bytes = by;
   return KFAC_OK;
 }
 
 extern "C" int kfac_profile_read(int id, double* total_ms, int64_t* launches) {
-  return kfac_profile_read_work(id, total_ms, launches, nullptr);
+  return kfac_profile_read_work(id, total_ms, launches, nullptr, nullptr);
 }
 
 // Every HIP object the library keeps across calls -- the inversion's cached graphs,

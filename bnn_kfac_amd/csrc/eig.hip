@@ -1006,11 +1006,11 @@ extern "C" int kfac_syev(const kfac_eig_job* jobs, int njobs, void* workspace, s
   hipStream_t st = (hipStream_t)stream;
   // profile slot with the tridiagonalisations' algorithmic bytes: each reflector reads
   // and rewrites the trailing rows once, sum_k (n - k)^2 x 16 B ~ 16 n^3 / 3
-  double work = 0.0;
+  double bytes = 0.0;
   if (prof_on())
     for (int i = 0; i < njobs; ++i)
-      if (jobs[i].n > EIG_LDS_MAX) work += 16.0 * (double)jobs[i].n * jobs[i].n * jobs[i].n / 3.0;
-  ProfScope ps(KFAC_PROF_SYEV, st, work);
+      if (jobs[i].n > EIG_LDS_MAX) bytes += 16.0 * (double)jobs[i].n * jobs[i].n * jobs[i].n / 3.0;
+  ProfScope ps(KFAC_PROF_SYEV, st, 0.0, bytes);
   EigArgs args{};
   char* ws = (char*)workspace;
   auto flush = [&]() -> int {

@@ -2014,6 +2014,15 @@ static int64_t job_krows(const kfac_factor_job& j) {
   if (job_ragged(j)) return j.x.rows * (j.nseg - 1) + j.x.last_rows;
   return j.x.rows * job_nseg(j);
 }
+// algorithmic bytes of a job's operand, read once: rows x cols x 4 (row-major, and the
+// channel-major grads: images x positions x channels), the images themselves for the
+// implicit im2col (images x C x H x W x 4)
+static double job_operand_bytes(const kfac_factor_job& j) {
+  const double rows = (double)job_krows(j);
+  if (j.x.layout == KFAC_PATCH)
+    return rows / (double)std::max<int64_t>(1, j.x.L) * (double)j.x.C * j.x.H * j.x.W * sizeof(float);
+  return rows * j.x.cols * sizeof(float);
+}
 
 // Split K so that the grouped launch fills the chip's workgroup slots (256 CUs x 4
 // resident workgroups) in as few dispatch rounds as possible with every task still
@@ -2325,10 +2334,13 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
                      : !staged ? KFAC_PROF_FACTOR_TILES
                      : (jobs[0].x.layout == KFAC_CHANNEL && cg.n <= 8 && !conv_small_off())
                          ? KFAC_PROF_FACTOR_CHANNEL_SMALL : KFAC_PROF_FACTOR_CONV;
-    double work = 0.0;
+    double work = 0.0, bytes = 0.0;
     if (prof_on())
-      for (int i = 0; i < njobs; ++i) work += (double)job_krows(jobs[i]) * factor_n(jobs[i]) * (factor_n(jobs[i]) + 1);
-    ProfScope ps(slot, stream, work);
+      for (int i = 0; i < njobs; ++i) {
+        work += (double)job_krows(jobs[i]) * factor_n(jobs[i]) * (factor_n(jobs[i]) + 1);
+        bytes += job_operand_bytes(jobs[i]);
+      }
+    ProfScope ps(slot, stream, work, bytes);
     switch (jobs[0].x.layout) {
       case KFAC_CHANNEL:
         if (staged)

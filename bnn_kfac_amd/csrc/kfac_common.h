@@ -31,16 +31,18 @@ static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // ---- optional launch timing (capi.hip): Prof scope records hipEvents around a launch
-// `work`: the launch's algorithmic flops (factor kernels: sum over jobs of K rows x
-// n(n+1), the lower triangle incl. the diagonal at 2 flops per product), summed per
+// `work` / `bytes`: the launch's algorithmic flops and HBM bytes (factor kernels: sum
+// over jobs of K rows x n (n + 1), and of the operand's bytes read once), summed per
 // slot by kfac_profile_read_work so a roofline names its own kernel's work
 bool prof_on();
-void prof_begin(int id, hipStream_t s, double work = 0.0);
+void prof_begin(int id, hipStream_t s, double work = 0.0, double bytes = 0.0);
 void prof_end(int id, hipStream_t s);
 struct ProfScope {
   int id;
   hipStream_t s;
-  ProfScope(int id_, hipStream_t s_, double work = 0.0) : id(id_), s(s_) { prof_begin(id, s, work); }
+  ProfScope(int id_, hipStream_t s_, double work = 0.0, double bytes = 0.0) : id(id_), s(s_) {
+    prof_begin(id, s, work, bytes);
+  }
   ~ProfScope() { prof_end(id, s); }
 };
 

@@ -334,16 +334,19 @@ KFAC_API int kfac_tri_unpack(const kfac_tri_job* jobs, int njobs, const float* p
  *     channel-major operand), 7 kfac_factor_channel_small (channel factors n <= 8),
  *   8 the whole kfac_syev call.
  * kfac_profile_read syncs the recorded events.  kfac_profile_read_work also
- * returns the slot's algorithmic work: for the factor slots (0, 4-7) the flops
- * sum_jobs K_rows * n (n + 1) of the launches (lower triangle incl. the diagonal,
- * 2 flops per product; curvatures.py:341-356), 0 for the others. */
+ * returns the slot's algorithmic work: `work` = flops, for the factor slots (0, 4-7)
+ * sum_jobs K_rows * n (n + 1) (lower triangle incl. the diagonal, 2 flops per
+ * product; curvatures.py:341-356); `bytes` = HBM bytes, for the factor slots each
+ * operand read once (rows x cols x 4; an im2col operand: its images), for the syev
+ * slot the tridiagonalisations' sum_k (n - k)^2 x 16 ~ 16 n^3 / 3 (n > 128). */
 enum kfac_prof_id { KFAC_PROF_FACTOR_TILES = 0, KFAC_PROF_FACTOR_REDUCE = 1, KFAC_PROF_INVERT = 2,
                     KFAC_PROF_QUAD_TILES = 3, KFAC_PROF_FACTOR_SYRK3 = 4, KFAC_PROF_FACTOR_X3 = 5,
                     KFAC_PROF_FACTOR_CONV = 6, KFAC_PROF_FACTOR_CHANNEL_SMALL = 7, KFAC_PROF_SYEV = 8,
                     KFAC_PROF_COUNT = 9 };
 KFAC_API int kfac_profile_enable(int on);
 KFAC_API int kfac_profile_read(int id, double* total_ms, int64_t* launches);
-KFAC_API int kfac_profile_read_work(int id, double* total_ms, int64_t* launches, double* work);
+KFAC_API int kfac_profile_read_work(int id, double* total_ms, int64_t* launches, double* work,
+                                   double* bytes);
 KFAC_API int kfac_profile_reset(void);
 
 /* ------------------------------------------------------------------- misc */

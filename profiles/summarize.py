@@ -1,17 +1,25 @@
 """Turn a profiles/collect.sh run (gpurun_out/prof_<tag>/) into the committed summaries.
 
-    python profiles/summarize.py r01          (r01_wide etc.: other configs, same recipe)
+    python profiles/summarize.py <tag> <config>      (config: mlp | lenet | wide)
 
 writes
-  profiles/<tag>/kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
-  profiles/<tag>/pmc_summary.json   per-kernel mean counter value per dispatch, every pass
-  profiles/factor_tiles_pmc.json    HBM bytes per kfac_factor_tiles launch (read by bench.py)
+  profiles/<tag>/kernel_stats.csv    rocprofv3 --kernel-trace --stats summary (verbatim)
+  profiles/<tag>/pmc_summary.json    per kernel family: mean counter value per dispatch,
+                                     every --pmc pass
+  profiles/pmc_<config>.json         per factor kernel family: HBM bytes per launch and
+                                     the trace's calls / mean launch time (bench.py reads
+                                     it for the roofline's `traffic`)
+
+A kernel FAMILY is the kernel's name without template arguments (and without the _t
+of the fp32 template kfac_factor_tiles_t): every instance of kfac_factor_conv<...>
+counts as one family, as the library's profile slot KFAC_PROF_FACTOR_CONV times them.
+The trace's figures per family are summed over instances (calls, total ns), so the
+family's mean launch time compares with the bench's `avg_launch_us` directly.
 
 HBM bytes follow MI355X_MICROARCH.md's rocprofv3 section: FETCH_SIZE and WRITE_SIZE
 come from separate passes (KiB units); on gfx950 FETCH_SIZE reports half the bytes of
-a wide (16 B/lane) coalesced read, so it is doubled.  Both the SYRK panel loads
-(global_load_lds_dwordx4 / global_load_dwordx4) and the slab stores are 16 B/lane or
-full 128-B rows.
+a wide coalesced read, so it is doubled (the x3 / syrk3 kernels' 4 B/lane buffer loads:
+the same x2, calibrated on a 512 MB operand read once, profiles/r03_x3/fetch_calib.txt).
 """
 import collections
 import csv
@@ -22,16 +30,19 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FETCH_X3_SCALE = 2.0  # FETCH_SIZE -> bytes for kfac_factor_tiles_x3's loads (see fetch_calib)
+FETCH_SCALE = 2.0
+FACTOR_FAMILIES = ("kfac_factor_tiles", "kfac_factor_tiles_x3", "kfac_factor_syrk3", "kfac_factor_conv",
+                   "kfac_factor_channel_small", "kfac_factor_reduce")
 
 
-def short(name):
-    """'void kfac::kfac_factor_tiles_t<32, 2, 2, 1>(kfac::FactorArgs)' -> 'kfac_factor_tiles'"""
+def family(name):
+    """'void kfac::kfac_factor_conv<2, 8, true, 2, false>(kfac::FactorArgs, kfac::ConvGeom)'
+    -> 'kfac_factor_conv'; 'kfac::t32::inv_step(...)' -> 't32::inv_step'."""
     base = name.split("(")[0].split("<")[0].replace("void ", "").replace("kfac::", "").strip()
     return base[:-2] if base.endswith("_t") else base
 
 
-def main(tag):
+def main(tag, config):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
@@ -40,50 +51,36 @@ def main(tag):
     for f in sorted(glob.glob(os.path.join(src, "pmc_*", "run_counter_collection.csv"))):
         vals = collections.defaultdict(list)
         for r in csv.DictReader(open(f)):
-            vals[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
+            vals[(family(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
         for (k, c), v in vals.items():
             pmc[k][c] = {"mean_per_dispatch": sum(v) / len(v), "dispatches": len(v)}
-    # the kernel-trace stats of the same bench command (mean launch time per kernel)
-    stats = {}
+    # the kernel-trace stats of the same bench command, summed over each family's instances
+    calls, total_ns = collections.Counter(), collections.Counter()
     for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
-        stats[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3}
+        calls[family(r["Name"])] += int(r["Calls"])
+        total_ns[family(r["Name"])] += float(r["TotalDurationNs"])
+    stats = {k: {"calls": calls[k], "avg_us": total_ns[k] / calls[k] / 1e3, "total_ms": total_ns[k] / 1e6}
+             for k in calls}
     with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
-        json.dump(pmc, f, indent=1, sort_keys=True)
-    # the dominant factor kernel of the run (most trace time): the fp32-MFMA SYRK, the
-    # split-pass bf16x3 SYRK (wide) or the register-split one (MNIST MLP)
-    cands = [k for k in ("kfac_factor_tiles", "kfac_factor_syrk3", "kfac_factor_tiles_x3")
-             if "FETCH_SIZE" in pmc.get(k, {}) and k in stats]
-    kname = max(cands, key=lambda k: stats[k]["calls"] * stats[k]["avg_us"]) if cands else "kfac_factor_tiles"
-    t = pmc.get(kname, {})
-    if "FETCH_SIZE" in t and "WRITE_SIZE" in t:
-        # FETCH_SIZE scale: x2 for 16 B/lane reads (MI355X_MICROARCH.md); the x3 kernel's
-        # 4 B/lane buffer loads are calibrated by tools/fetch_calib.py (FETCH_X3_SCALE)
-        # (round 5: kfac_factor_syrk3 splits in the workgroup and reads fp32 rows by the
-        # same 4 B/lane buffer loads as the x3 kernel)
-        scale = FETCH_X3_SCALE if kname in ("kfac_factor_tiles_x3", "kfac_factor_syrk3") else 2.0
-        fetch = t["FETCH_SIZE"]["mean_per_dispatch"] * 1024 * scale
+        json.dump({"trace": stats, "pmc": pmc}, f, indent=1, sort_keys=True)
+    kernels = {}
+    for k in FACTOR_FAMILIES:
+        t = pmc.get(k, {})
+        if "FETCH_SIZE" not in t or "WRITE_SIZE" not in t:
+            continue
+        fetch = t["FETCH_SIZE"]["mean_per_dispatch"] * 1024 * FETCH_SCALE
         write = t["WRITE_SIZE"]["mean_per_dispatch"] * 1024
-        note = (f"FETCH_SIZE x{scale:g} (gfx950 read-width correction) + WRITE_SIZE, KiB->bytes, "
-                "mean over the bench's launches (15 updates per pass, last batch short)")
-        if kname == "kfac_factor_syrk3":
-            note += ("; kfac_factor_syrk3 (round 5: split in the workgroup, no split pass) reads "
-                     "fp32 operand rows by buffer_load_dword (4 B/lane), scale as for the x3 kernel")
-        if kname == "kfac_factor_tiles_x3":
-            note += ("; kfac_factor_tiles_x3 reads fp32 operand rows by buffer_load_dword "
-                     "(4 B/lane, 128 B per half-wave): scale calibrated on a 512 MB operand "
-                     "read once (profiles/r03_x3/fetch_calib.txt)")
-        out = {"kernel": kname, "tag": tag, "fetch_bytes_per_launch": fetch,
-               "write_bytes_per_launch": write, "hbm_bytes_per_launch": fetch + write,
-               "rocprof_trace": stats.get(kname), "note": note}
-        with open(os.path.join(dst, "factor_tiles_hbm.json"), "w") as f:
-            json.dump(out, f, indent=1)
-        # the files bench.py reads: factor_tiles_pmc.json for the headline (MLP) profile,
-        # factor_tiles_pmc_<config>.json for r02_<config> etc.
-        name = "factor_tiles_pmc.json" if "_" not in tag else f"factor_tiles_pmc_{tag.split('_', 1)[1]}.json"
-        with open(os.path.join(ROOT, "profiles", name), "w") as f:
-            json.dump(out, f, indent=1)
-        print(json.dumps(out, indent=1))
+        kernels[k] = {"fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
+                      "hbm_bytes_per_launch": fetch + write, "fetch_scale": FETCH_SCALE,
+                      "pmc_dispatches": t["FETCH_SIZE"]["dispatches"], "rocprof_trace": stats.get(k)}
+    out = {"tag": tag, "config": config, "kernels": kernels,
+           "note": "per kernel family: FETCH_SIZE x2 (gfx950 read-width correction) + WRITE_SIZE, KiB -> "
+                   "bytes, mean per dispatch over the bench run's launches (separate --pmc passes); "
+                   "rocprof_trace = the same command's kernel trace, summed over the family's instances"}
+    with open(os.path.join(ROOT, "profiles", f"pmc_{config}.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "mlp")
