@@ -446,8 +446,14 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, const fl
 // path (or the narrow direct-load path), and the ring is all the LDS (32 KB, not the
 // register-staged path's 34 KB): 4 resident workgroups leave 32 KB of a CU's 160,
 // room for a 32-tile inversion workgroup (29 KB) of an overlapped invert().
-// start delay per dispatch round (blockIdx / 256), in 512-cycle s_sleep(8) units
-constexpr int STAGGER = 5;
+// Start delay per dispatch round (blockIdx / 256), in 512-cycle s_sleep(8) units: the
+// workgroups that share a CU start ~1 us apart, so their load / barrier stalls
+// interleave instead of coinciding (fp32 LDS-DMA SYRK: +2.5 %).  A design
+// constant, not a timing build.
+#ifndef KFAC_STAGGER
+#define KFAC_STAGGER 5
+#endif
+constexpr int STAGGER = KFAC_STAGGER;
 
 template <int GBK, int NSLOT, bool GLDS_ONLY = false, int FAMILY = KFAC_ROWMAJOR>
 __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs args) {
@@ -1315,7 +1321,8 @@ __device__ __forceinline__ void factor_task_x3(const FactorJobDev& J, const floa
 __global__ __launch_bounds__(X3_THREADS, 2) void kfac_factor_tiles_x3(FactorArgs args) {
   // (LDS only for the epilogue's hand-off: a block row, 16 KB; a pair's blocks, 20 KB)
   __shared__ __attribute__((aligned(16))) float lds[5 * 16 * 64];
-  for (int i = 0; i < STAGGER * (int)(blockIdx.x >> 8); ++i) __builtin_amdgcn_s_sleep(8);
+  // (no start stagger here: the fp32 kernel's +2.5 % measured neutral on this one, MLP
+  // line 1.951-1.954e8 without vs 1.951-1.957e8 with, 3 alternating runs, profiles/r06b/)
   const int task = xcd_task(blockIdx.x, gridDim.x);
   int j = 0;
   while (j + 1 < args.njobs && task >= args.task_end[j]) ++j;
@@ -1354,6 +1361,13 @@ constexpr int CONV_SRC_MAX = 2048;   // per-image staged elements (PATCH) / floa
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int CONV_CB = 2;  // 32x32 blocks per wave (mode 0): 4*CONV_CB per workgroup
+// operand chunk of the two-block row loop: 2 steps ahead (4 MFMAs of 64 cycles cover the
+// LDS latency) instead of 4 keeps the PATCH instances inside the 128-VGPR budget of 4
+// workgroups per CU without spilling (LeNet-5: conv 2.90 vs 3.04 ms per pass, 1.69 vs
+// 1.63e7 img/s, 3 alternating runs, profiles/r06b/)
+#ifndef CONV_CK2
+#define CONV_CK2 2
+#endif
 
 struct ConvGeom {
   int mode;        // 0: 64x64 tiles, 1: narrow 32x32, 2: narrow 16x16
@@ -1520,7 +1534,7 @@ __global__ __launch_bounds__(NTHREADS, (CB == 2 && !M3) ? KFAC_CONV_OCC : 4) voi
   // two blocks (CB = 2) of one row group: operands for CK steps of both blocks per
   // chunk, double-buffered as in row_mfmas, MFMAs alternating between the blocks
   auto row_mfmas2 = [&](const float* pa0, const float* pb0, const float* pa1, const float* pb1) {
-    constexpr int CK = 4;
+    constexpr int CK = CONV_CK2;
     const int st = STRIDE1 ? 1 : cg.stride, T = cg.T, last = (T - 1) * st;
     float ca[2][CK], cb[2][CK], na[2][CK], nb[2][CK];
 #pragma unroll
