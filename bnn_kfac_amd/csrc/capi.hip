@@ -39,6 +39,7 @@ Knobs g_knobs = [] {
   k.tiles_x3 = env_mode("KFAC_TILES_X3");
   k.conv_small = env_int("KFAC_CONV_SMALL", 1) != 0;
   k.conv_k = std::max(0, env_int("KFAC_CONV_K", 0));
+  k.conv_x3 = env_int("KFAC_CONV_X3", 1) != 0;
   k.inv_graph = env_int("KFAC_INV_GRAPH", 1) != 0;
   k.inv_lookahead = env_int("KFAC_INV_LOOKAHEAD", 1) != 0;
   k.eig_g = std::max(0, env_int("KFAC_EIG_G", 0));
@@ -70,6 +71,7 @@ extern "C" int kfac_get_knob(const char* name, int* value) {
   else if (!strcmp(name, "KFAC_TILES_X3")) *value = k.tiles_x3;
   else if (!strcmp(name, "KFAC_CONV_SMALL")) *value = k.conv_small;
   else if (!strcmp(name, "KFAC_CONV_K")) *value = k.conv_k;
+  else if (!strcmp(name, "KFAC_CONV_X3")) *value = k.conv_x3;
   else if (!strcmp(name, "KFAC_INV_GRAPH")) *value = k.inv_graph;
   else if (!strcmp(name, "KFAC_INV_LOOKAHEAD")) *value = k.inv_lookahead;
   else if (!strcmp(name, "KFAC_EIG_G")) *value = k.eig_g;

@@ -1388,6 +1388,16 @@ struct ConvGeom {
   int src;         // staged source elements (PATCH) / float4s (CHANNEL) per image
   int nq;          // mode 0: 32x32 blocks of the factor's lower triangle
   int units;       // workgroups per K-split (mode 0: ceil(nq / (4*CONV_CB)) block groups; else 1)
+  // mode 4 (kfac_factor_conv_x3: im2col operand split into bf16x3 in LDS)
+  int nb;          // 32-blocks per factor edge (im2col rows padded to 32 nb)
+  int L;           // output positions per image (Ho * Wo)
+  int Wo, sh, sw;  // output row length, strides
+  int LPC;         // positions per chunk (multiple of 16): an image is ceil(L / LPC) chunks
+  int nch;         // chunks per image
+  int pitch;       // bf16 elements per im2col row (LPC + 8: 16-byte reads conflict-free)
+  int imgf;        // floats of one staged fp32 image (C padded planes)
+  int ones;        // bias column (-1: none)
+  int ldsb;        // bytes of dynamic LDS
 };
 
 #ifndef KFAC_CONV_OCC
@@ -1712,6 +1722,186 @@ __global__ __launch_bounds__(NTHREADS, (CB == 2 && !M3) ? KFAC_CONV_OCC : 4) voi
   }
 }
 
+// ------------------------------------------- conv factors in bf16x3 (mode 4)
+// The im2col factor of a conv layer (PATCH operand, n > 32: LeNet-5's conv2 A, n = 151
+// over 100 positions per image), F = sum over (image, position) P[pos]^T P[pos]
+// (curvatures.py:341-343), on the bf16 MFMA at six products per fp32 product (the
+// exact three-part split of the x3 / syrk3 kernels: 417 TF/s fp32-equivalent against
+// the fp32 MFMA's 157).  One workgroup of 8 waves per CU takes whole images; per image
+// (and chunk of its positions) it
+//   1. stages the fp32 image in LDS with its zero padding (the next image's loads in
+//      flight during the current one's MFMAs);
+//   2. builds the chunk's explicit im2col in LDS, split ONCE into its three bf16 parts,
+//      laid out [part][feature][position] with positions contiguous: an MFMA fragment --
+//      8 consecutive positions of one feature -- is one ds_read_b128 (row pitch
+//      LPC + 8 bf16: the 16-byte reads of a lane group hit distinct bank quads);
+//   3. each wave multiplies its 32 x 32 blocks of the factor's lower triangle (block
+//      b = wave + 8 i), six v_mfma_f32_32x32x16_bf16 per block and 16 positions.
+// The register-gathered fp32 path (kfac_factor_conv mode 0) paid two LDS reads per
+// 32x32x2 fp32 MFMA at 1/16 of the bf16 rate.  Partials go to the same slab tiles.
+constexpr int CX3_THREADS = 512;
+constexpr int CX3_WAVES = CX3_THREADS / 64;
+constexpr int CX3_PM = CONV_SRC_MAX / CX3_THREADS;  // staged source elements per thread
+
+template <int BPW>
+__global__ __launch_bounds__(CX3_THREADS, 1) void kfac_factor_conv_x3(FactorArgs args, ConvGeom cg) {
+  extern __shared__ __attribute__((aligned(16))) char cx3[];
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const int task = xcd_task(blockIdx.x, gridDim.x);
+  int jx = 0;
+  while (jx + 1 < args.njobs && task >= args.task_end[jx]) ++jx;
+  const FactorJobDev& J = args.job[jx];
+  const OpDev& op = J.x;
+  const int split = task - J.task_begin;  // one unit: task = split
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t b0 = (int64_t)split * cg.B / J.splits, b1 = (int64_t)(split + 1) * cg.B / J.splits;
+  const int NR = 32 * cg.nb;              // im2col rows (features padded to 32 nb)
+  const int partb = NR * cg.pitch * 2;    // bytes of one bf16 part
+  char* col = cx3;                        // [3][NR][pitch] bf16
+  // two fp32 image buffers (imgf floats each), then a zero region of imgf floats: an
+  // invalid position (past L) reads zero region + feature offset (< imgf)
+  float* img = reinterpret_cast<float*>(cx3 + 3 * partb);
+  int* posoff = reinterpret_cast<int*>(img + 3 * cg.imgf);  // nch * LPC positions (-1: past L)
+  int* featoff = posoff + cg.nch * cg.LPC;                  // n features
+  // once per task: zero the im2col (padded feature rows, pitch slack) and the image
+  // area (pad cells, zero region); the position and feature offset tables
+  for (int e = tid; e < 3 * partb / 16; e += CX3_THREADS)
+    reinterpret_cast<u32x4*>(col)[e] = u32x4{0u, 0u, 0u, 0u};
+  for (int e = tid; e < 3 * cg.imgf; e += CX3_THREADS) img[e] = 0.f;
+  for (int q = tid; q < cg.nch * cg.LPC; q += CX3_THREADS) {
+    const int oh = q / cg.Wo, ow = q - oh * cg.Wo;
+    posoff[q] = q < cg.L ? oh * cg.sh * cg.Wp + ow * cg.sw : -1;
+  }
+  for (int f = tid; f < cg.n; f += CX3_THREADS) {
+    const int kk = op.kh * op.kw, c = f / kk, r = f - c * kk, ki = r / op.kw, kj = r - ki * op.kw;
+    featoff[f] = f < op.cols ? c * cg.plane + ki * cg.Wp + kj : 0;  // (the ones column: selected)
+  }
+  // staging map of this thread's source elements (image (c, h, w) -> padded plane)
+  int dmap[CX3_PM];
+#pragma unroll
+  for (int q = 0; q < CX3_PM; ++q) {
+    const int e = tid + q * CX3_THREADS;
+    int d = -1;
+    if (e < cg.src) {
+      const int hw = op.H * op.W, c = e / hw, r = e - c * hw, h = r / op.W, w = r - h * op.W;
+      d = c * cg.plane + (h + op.ph) * cg.Wp + (w + op.pw);
+    }
+    dmap[q] = d;
+  }
+  float pre[CX3_PM];
+  auto fetch = [&](int64_t b) {
+    const int seg = (int)((uint32_t)b / (uint32_t)cg.bseg);
+    const float* src = seg_base(J, args.segs, seg) + (b - (int64_t)seg * cg.bseg) * op.sB;
+#pragma unroll
+    for (int q = 0; q < CX3_PM; ++q)
+      if (dmap[q] >= 0) pre[q] = src[tid + q * CX3_THREADS];
+  };
+  auto commit = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < CX3_PM; ++q)
+      if (dmap[q] >= 0) img[buf + dmap[q]] = pre[q];
+  };
+  // this wave's blocks of the lower triangle and its lanes' fragment offsets
+  const int m = lane & 31, hh = lane >> 5;
+  int offA[BPW], offB[BPW];
+  bool diag[BPW];
+  int nmine = 0;
+#pragma unroll
+  for (int i = 0; i < BPW; ++i) {
+    const int b = wave + CX3_WAVES * i;
+    int bi = 0, bj = 0;
+    if (b < cg.nq) {
+      tri_decode(b, bi, bj);
+      ++nmine;
+    }
+    offA[i] = ((32 * bi + m) * cg.pitch + 8 * hh) * 2;
+    offB[i] = ((32 * bj + m) * cg.pitch + 8 * hh) * 2;
+    diag[i] = bi == bj;
+  }
+  floatx16 acc[BPW];
+#pragma unroll
+  for (int i = 0; i < BPW; ++i)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[i][v] = 0.f;
+  // build: thread (g, fi) makes 8 positions (group g of the chunk) of features fi,
+  // fi + FS, ...: 8 fp32 LDS reads, the split, three 16-byte stores
+  const int G8 = cg.LPC / 8, FS = CX3_THREADS / G8;
+  const int g = tid % G8, fi = tid / G8;
+  auto build = [&](int buf, int c) {
+    if (fi >= FS) return;
+    const int q0 = c * cg.LPC + 8 * g;
+    int po[8];
+    bool valid[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int pq = posoff[q0 + e];
+      valid[e] = pq >= 0;
+      po[e] = valid[e] ? buf + pq : 2 * cg.imgf;
+    }
+    for (int f = fi; f < cg.n; f += FS) {
+      const int fo = featoff[f];
+      const bool one = f == cg.ones;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x = img[po[e] + fo];
+        v[e] = one ? (valid[e] ? 1.f : 0.f) : x;
+      }
+      const X3Frag fr = x3_split8(v);
+      char* dst = col + (f * cg.pitch + 8 * g) * 2;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<bf16x8*>(dst + p * partb) = fr.p[p];
+    }
+  };
+  auto frag = [&](int off, X3Frag& fr) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) fr.p[p] = *reinterpret_cast<const bf16x8*>(col + p * partb + off);
+  };
+  auto mma = [&](int c) {
+    const int kst = (min(cg.LPC, cg.L - c * cg.LPC) + 15) / 16;  // 16-position k-steps
+    for (int s = 0; s < kst; ++s) {
+#pragma unroll
+      for (int i = 0; i < BPW; ++i) {
+        if (i >= nmine) break;
+        X3Frag A, B;
+        frag(offA[i] + 32 * s, A);
+        if (diag[i]) B = A;
+        else frag(offB[i] + 32 * s, B);
+        x3_six(acc[i], A, B);
+      }
+    }
+  };
+
+  if (b0 < b1) fetch(b0);
+  __syncthreads();  // (the zero fill before the first commit)
+  if (b0 < b1) commit(0);
+  for (int64_t b = b0; b < b1; ++b) {
+    const int buf = (int)((b - b0) & 1) * cg.imgf;
+    for (int c = 0; c < cg.nch; ++c) {
+      __syncthreads();  // image b committed; every wave done reading the previous im2col
+      if (c == 0 && b + 1 < b1) fetch(b + 1);  // next image's loads fly during this one
+      build(buf, c);
+      __syncthreads();
+      // (the other buffer was last read by the previous image's builds, before the
+      // barrier above)
+      if (c == cg.nch - 1 && b + 1 < b1) commit(cg.imgf - buf);
+      mma(c);
+    }
+  }
+  // block (bi, bj) = quadrant (bi & 1, bj & 1) of slab tile (bi / 2, bj / 2)
+#pragma unroll
+  for (int i = 0; i < BPW; ++i) {
+    if (i >= nmine) break;
+    int bi, bj;
+    tri_decode(wave + CX3_WAVES * i, bi, bj);
+    const int ti = bi >> 1, tj = bj >> 1;
+    float* o = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.sstride + split) * TILE * TILE +
+               (bi & 1) * 32 * TILE + (bj & 1) * 32;
+    put_partial(J, acc[i], [&](int v) { return &o[acc_row(v, lane) * TILE + (lane & 31)]; });
+  }
+}
+
 // Channel-major factors with n <= 8 (the G of a conv layer with few output
 // channels, e.g. LeNet-5's conv1: 6): F = sum over (image, position) of g g^T is
 // n(n+1)/2 FMAs per position against n loads -- an HBM stream, not MFMA work.  Each
@@ -1802,6 +1992,45 @@ static bool conv_small_off() { return !knobs().conv_small; }
 // Geometry of a conv job on the LDS-staged kernel; false: the job takes the
 // register-staged path (images too large, channel blocks not float4-shaped, or an
 // empty batch).  A multi-batch job's images are its nseg batches' images in order.
+// LDS of the mode-4 workgroup: at most 131 KB, so a 29 KB inversion workgroup of an
+// overlapped invert() still fits on the CU (160 KB)
+constexpr int CX3_LDS_MAX = 134144;
+
+// Mode 4 (kfac_factor_conv_x3): an im2col operand with n > 32 whose padded image and
+// im2col chunk fit the LDS; positions per chunk LPC as large as fits (one chunk per
+// image when the whole image does).
+static bool conv_x3_geom(const kfac_operand& o, ConvGeom& g) {
+  const int n = g.n;
+  if (n <= 32 || (int64_t)o.C * o.H * o.W > CONV_SRC_MAX || o.sh <= 0 || o.sw <= 0) return false;
+  g.nb = (int)cdiv(n, 32);
+  g.nq = g.nb * (g.nb + 1) / 2;
+  if (g.nq > 4 * CX3_WAVES) return false;  // (BPW <= 4 blocks per wave)
+  g.Wp = o.W + 2 * o.pw;
+  g.plane = (o.H + 2 * o.ph) * g.Wp;
+  g.imgf = o.C * g.plane;
+  g.L = (int)o.L;
+  g.Wo = o.Wo;
+  g.sh = o.sh;
+  g.sw = o.sw;
+  g.src = o.C * o.H * o.W;
+  g.ones = o.has_ones ? o.cols : -1;
+  for (int lpc = (int)cdiv(o.L, 16) * 16; lpc >= 16; lpc -= 16) {
+    const int nch = (int)cdiv(o.L, lpc), pitch = lpc + 8;
+    const int64_t bytes = (int64_t)3 * 32 * g.nb * pitch * 2 + (int64_t)4 * 3 * g.imgf +
+                          (int64_t)4 * ((int64_t)nch * lpc + n);
+    if (bytes <= CX3_LDS_MAX && lpc / 8 <= CX3_THREADS) {
+      g.LPC = lpc;
+      g.nch = nch;
+      g.pitch = pitch;
+      g.ldsb = (int)bytes;
+      g.mode = 4;
+      g.units = 1;
+      return true;
+    }
+  }
+  return false;
+}
+
 static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
   const kfac_operand& o = j.x;
   const int64_t nseg = j.nseg > 1 ? j.nseg : 1;
@@ -1811,13 +2040,14 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
   const int n = o.cols + (o.has_ones ? 1 : 0);
   g = ConvGeom{};
   g.n = n;
+  g.bseg = (int)(o.rows / o.L);
+  g.B = (int)(nseg * g.bseg);
+  if (o.layout == KFAC_PATCH && knobs().conv_x3 && conv_x3_geom(o, g)) return true;
 #ifndef KFAC_CONV_NARROW32
 #define KFAC_CONV_NARROW32 3  // n in 17..32: 3 = three 16x16 blocks, 1 = one 32x32 block (A/B)
 #endif
   g.mode = n <= 16 ? 2 : (n <= 32 ? KFAC_CONV_NARROW32 : 0);
   g.KR = g.mode >= 2 ? 4 : 2;
-  g.bseg = (int)(o.rows / o.L);
-  g.B = (int)(nseg * g.bseg);
   int64_t lds;
   // Bank-conflict-free operand reads: an MFMA's 32 lanes of one lane group read 32
   // consecutive factor columns, column (c, ki, kj) at c*plane + ki*Wp + kj (PATCH) or
@@ -1886,8 +2116,27 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
   return true;
 }
 
+template <int BPW>
+static bool launch_conv_x3(const FactorArgs& args, const ConvGeom& g, int tasks, hipStream_t stream) {
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&kfac_factor_conv_x3<BPW>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               CX3_LDS_MAX) == hipSuccess;
+  if (!attr) return false;
+  hipLaunchKernelGGL(kfac_factor_conv_x3<BPW>, dim3(tasks), dim3(CX3_THREADS), (size_t)g.ldsb, stream, args, g);
+  return true;
+}
+
 template <int LAYOUT>
 static void launch_conv(const FactorArgs& args, const ConvGeom& g, int tasks, hipStream_t stream) {
+  if (g.mode == 4) {
+    const int bpw = (g.nq + CX3_WAVES - 1) / CX3_WAVES;
+    const bool ok = bpw <= 1 ? launch_conv_x3<1>(args, g, tasks, stream)
+                  : bpw == 2 ? launch_conv_x3<2>(args, g, tasks, stream)
+                  : bpw == 3 ? launch_conv_x3<3>(args, g, tasks, stream)
+                             : launch_conv_x3<4>(args, g, tasks, stream);
+    (void)ok;  // (a failed attribute surfaces as the launch error below)
+    return;
+  }
   if (LAYOUT == KFAC_CHANNEL && g.n <= 8 && !conv_small_off()) {
     // the exact channel count (LeNet-5 conv1: 6) sizes the register triangle and its
     // reduction; other counts take the next instance up (their extra rows are zero)
@@ -2202,8 +2451,9 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
       // (the n <= 8 channel kernel: half the slots -- its per-task reduction is the
       // larger cost there: conv1 G 15.7 / 12.4 / 13.2 us at k = 1 / 2 / 4)
       const bool small = jobs[i].x.layout == KFAC_CHANNEL && cg.n <= 8 && !conv_small_off();
-      // (mode-0 instances are compiled for KFAC_CONV_OCC resident workgroups per CU)
-      const int64_t cslots = cg.mode == 0 ? (int64_t)KFAC_CONV_OCC * 256 : slots;
+      // (mode-0 instances are compiled for KFAC_CONV_OCC resident workgroups per CU;
+      // mode 4 runs one 512-thread workgroup per CU)
+      const int64_t cslots = cg.mode == 0 ? (int64_t)KFAC_CONV_OCC * 256 : cg.mode == 4 ? 256 : slots;
       int k = (int)std::max<int64_t>(1, cdiv((int64_t)cg.units * cg.B, small ? cslots / 2 : cslots));
       if (knobs().conv_k > 0) k = knobs().conv_k;
       k = std::min(k, cg.B);
@@ -2347,7 +2597,8 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
     const int slot = s3 ? KFAC_PROF_FACTOR_SYRK3 : x3 ? KFAC_PROF_FACTOR_X3
                      : !staged ? KFAC_PROF_FACTOR_TILES
                      : (jobs[0].x.layout == KFAC_CHANNEL && cg.n <= 8 && !conv_small_off())
-                         ? KFAC_PROF_FACTOR_CHANNEL_SMALL : KFAC_PROF_FACTOR_CONV;
+                         ? KFAC_PROF_FACTOR_CHANNEL_SMALL
+                     : cg.mode == 4 ? KFAC_PROF_FACTOR_CONV_X3 : KFAC_PROF_FACTOR_CONV;
     double work = 0.0, bytes = 0.0;
     if (prof_on())
       for (int i = 0; i < njobs; ++i) {

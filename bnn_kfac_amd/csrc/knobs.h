@@ -14,6 +14,7 @@ struct Knobs {
   int tiles_x3;    // KFAC_TILES_X3: kfac_factor_tiles_x3 (auto: largest n >= 512)
   int conv_small;  // KFAC_CONV_SMALL: channel factors with n <= 8 on kfac_factor_channel_small (1)
   int conv_k;      // KFAC_CONV_K: images per conv task (0: the planner's)
+  int conv_x3;     // KFAC_CONV_X3: im2col factors with n > 32 on kfac_factor_conv_x3 (bf16x3) (1)
   // per call (kfac_set_knob may change them between calls)
   int inv_graph;      // KFAC_INV_GRAPH: replay the merged inversion steps from a cached hipGraph (1)
   int inv_lookahead;  // KFAC_INV_LOOKAHEAD: large inversions' bulk update split over a helper stream (1)
