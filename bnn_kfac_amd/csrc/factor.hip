@@ -1398,6 +1398,7 @@ struct ConvGeom {
   int imgf;        // floats of one staged fp32 image (C padded planes)
   int ones;        // bias column (-1: none)
   int ldsb;        // bytes of dynamic LDS
+  int kw;          // waves per block (nq <= 4: the block's k-steps interleaved over kw waves)
 };
 
 #ifndef KFAC_CONV_OCC
@@ -1727,18 +1728,28 @@ __global__ __launch_bounds__(NTHREADS, (CB == 2 && !M3) ? KFAC_CONV_OCC : 4) voi
 // over 100 positions per image), F = sum over (image, position) P[pos]^T P[pos]
 // (curvatures.py:341-343), on the bf16 MFMA at six products per fp32 product (the
 // exact three-part split of the x3 / syrk3 kernels: 417 TF/s fp32-equivalent against
-// the fp32 MFMA's 157).  One workgroup of 8 waves per CU takes whole images; per image
-// (and chunk of its positions) it
-//   1. stages the fp32 image in LDS with its zero padding (the next image's loads in
-//      flight during the current one's MFMAs);
-//   2. builds the chunk's explicit im2col in LDS, split ONCE into its three bf16 parts,
-//      laid out [part][feature][position] with positions contiguous: an MFMA fragment --
-//      8 consecutive positions of one feature -- is one ds_read_b128 (row pitch
-//      LPC + 8 bf16: the 16-byte reads of a lane group hit distinct bank quads);
-//   3. each wave multiplies its 32 x 32 blocks of the factor's lower triangle (block
-//      b = wave + 8 i), six v_mfma_f32_32x32x16_bf16 per block and 16 positions.
-// The register-gathered fp32 path (kfac_factor_conv mode 0) paid two LDS reads per
-// 32x32x2 fp32 MFMA at 1/16 of the bf16 rate.  Partials go to the same slab tiles.
+// the fp32 MFMA's 157).  One workgroup of 8 waves per CU takes whole images (a large
+// image in chunks of LPC positions).  Per image it
+//   * stages the fp32 image in LDS with its zero padding (the next image's loads fly
+//     during the current one, its copy goes into the other of two image buffers);
+//   * builds the explicit im2col in LDS, split ONCE into its three bf16 parts, laid out
+//     [part][feature][position] with positions contiguous: an MFMA fragment -- 8
+//     consecutive positions of one feature -- is one ds_read_b128 (row pitch LPC + 8
+//     bf16: the 16-byte reads of a lane group hit distinct bank quads).  A thread owns
+//     one 8-position group and every FS-th feature, so the lanes of a wave gather
+//     consecutive features (neighbouring words; positions fastest gave 3-4-way bank
+//     conflicts and 6 % more time, profiles/r06h/);
+//   * multiplies: each wave its 32 x 32 blocks of the lower triangle (block b = wave +
+//     8 i), six v_mfma_f32_32x32x16_bf16 per block and 16 positions, the next k-step's
+//     fragments read during the current one's MFMAs.
+// One im2col buffer (115 KB for conv2 A), so the build and the MFMAs of an image are
+// two barrier-separated phases.  Tried: two buffers of half the positions with waves
+// 0-3 building while waves 4-7 multiply (and the other way round): 389 vs 306 us per
+// launch -- the 48-position chunks cost more per-chunk overhead than the overlap saved
+// (profiles/r06g/).  Partials go to the slab tiles of the other conv paths.
+#ifndef CX3_PIPE
+#define CX3_PIPE 1
+#endif
 constexpr int CX3_THREADS = 512;
 constexpr int CX3_WAVES = CX3_THREADS / 64;
 constexpr int CX3_PM = CONV_SRC_MAX / CX3_THREADS;  // staged source elements per thread
@@ -1758,24 +1769,24 @@ __global__ __launch_bounds__(CX3_THREADS, 1) void kfac_factor_conv_x3(FactorArgs
   const int64_t b0 = (int64_t)split * cg.B / J.splits, b1 = (int64_t)(split + 1) * cg.B / J.splits;
   const int NR = 32 * cg.nb;              // im2col rows (features padded to 32 nb)
   const int partb = NR * cg.pitch * 2;    // bytes of one bf16 part
-  char* col = cx3;                        // [3][NR][pitch] bf16
+  char* colbuf = cx3;                     // [3][NR][pitch] bf16
   // two fp32 image buffers (imgf floats each), then a zero region of imgf floats: an
   // invalid position (past L) reads zero region + feature offset (< imgf)
   float* img = reinterpret_cast<float*>(cx3 + 3 * partb);
   int* posoff = reinterpret_cast<int*>(img + 3 * cg.imgf);  // nch * LPC positions (-1: past L)
-  int* featoff = posoff + cg.nch * cg.LPC;                  // n features
+  int* featoff = posoff + cg.nch * cg.LPC;                  // cols features
   // once per task: zero the im2col (padded feature rows, pitch slack) and the image
   // area (pad cells, zero region); the position and feature offset tables
   for (int e = tid; e < 3 * partb / 16; e += CX3_THREADS)
-    reinterpret_cast<u32x4*>(col)[e] = u32x4{0u, 0u, 0u, 0u};
+    reinterpret_cast<u32x4*>(colbuf)[e] = u32x4{0u, 0u, 0u, 0u};
   for (int e = tid; e < 3 * cg.imgf; e += CX3_THREADS) img[e] = 0.f;
   for (int q = tid; q < cg.nch * cg.LPC; q += CX3_THREADS) {
     const int oh = q / cg.Wo, ow = q - oh * cg.Wo;
     posoff[q] = q < cg.L ? oh * cg.sh * cg.Wp + ow * cg.sw : -1;
   }
-  for (int f = tid; f < cg.n; f += CX3_THREADS) {
+  for (int f = tid; f < op.cols; f += CX3_THREADS) {
     const int kk = op.kh * op.kw, c = f / kk, r = f - c * kk, ki = r / op.kw, kj = r - ki * op.kw;
-    featoff[f] = f < op.cols ? c * cg.plane + ki * cg.Wp + kj : 0;  // (the ones column: selected)
+    featoff[f] = c * cg.plane + ki * cg.Wp + kj;
   }
   // staging map of this thread's source elements (image (c, h, w) -> padded plane)
   int dmap[CX3_PM];
@@ -1802,16 +1813,19 @@ __global__ __launch_bounds__(CX3_THREADS, 1) void kfac_factor_conv_x3(FactorArgs
     for (int q = 0; q < CX3_PM; ++q)
       if (dmap[q] >= 0) img[buf + dmap[q]] = pre[q];
   };
-  // this wave's blocks of the lower triangle and its lanes' fragment offsets
+  // this wave's blocks of the lower triangle and its lanes' fragment offsets: blocks
+  // wave + 8 i, or (few blocks, kw > 1) block wave / kw over every kw-th k-step
   const int m = lane & 31, hh = lane >> 5;
+  const int KW = cg.kw, kp = wave % KW;
+  auto block_of = [&](int i) { return KW > 1 ? wave / KW : wave + CX3_WAVES * i; };
   int offA[BPW], offB[BPW];
   bool diag[BPW];
   int nmine = 0;
 #pragma unroll
   for (int i = 0; i < BPW; ++i) {
-    const int b = wave + CX3_WAVES * i;
+    const int b = block_of(i);
     int bi = 0, bj = 0;
-    if (b < cg.nq) {
+    if (b < cg.nq && (KW == 1 || i == 0)) {
       tri_decode(b, bi, bj);
       ++nmine;
     }
@@ -1824,77 +1838,136 @@ __global__ __launch_bounds__(CX3_THREADS, 1) void kfac_factor_conv_x3(FactorArgs
   for (int i = 0; i < BPW; ++i)
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[i][v] = 0.f;
-  // build: thread (g, fi) makes 8 positions (group g of the chunk) of features fi,
-  // fi + FS, ...: 8 fp32 LDS reads, the split, three 16-byte stores
-  const int G8 = cg.LPC / 8, FS = CX3_THREADS / G8;
-  const int g = tid % G8, fi = tid / G8;
-  auto build = [&](int buf, int c) {
-    if (fi >= FS) return;
+
+  // build chunk c of the image in fp32 buffer `buf` into im2col buffer `col`.  Thread t
+  // owns the 8-position group g = t / FS of the chunk and features fi, fi + FS, ...
+  // (fi = t % FS, FS = 512 / (LPC / 8)): lanes of a wave take consecutive FEATURES of
+  // one group, so their fp32 gathers hit neighbouring words; the group's positions are
+  // resolved once per chunk.  Only the k-steps holding valid positions are built (a
+  // short last chunk builds few: the groups its MFMAs read, past-L positions as zeros --
+  // the buffer still holds an earlier chunk beyond them).
+  const int FS = CX3_THREADS / (cg.LPC / 8);
+  const int g = tid / FS, fi = tid - g * FS;
+  auto build = [&](char* col, int buf, int c) {
+    const int valid_pos = min(cg.LPC, cg.L - c * cg.LPC);
+    const int groups = 2 * ((valid_pos + 15) / 16);
+    if (g >= groups) return;
     const int q0 = c * cg.LPC + 8 * g;
     int po[8];
-    bool valid[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int pq = posoff[q0 + e];
-      valid[e] = pq >= 0;
-      po[e] = valid[e] ? buf + pq : 2 * cg.imgf;
+      po[e] = pq >= 0 ? buf + pq : 2 * cg.imgf;
     }
-    for (int f = fi; f < cg.n; f += FS) {
+    char* dstg = col + 16 * g;
+    for (int f = fi; f < op.cols; f += FS) {
       const int fo = featoff[f];
-      const bool one = f == cg.ones;
       float v[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float x = img[po[e] + fo];
-        v[e] = one ? (valid[e] ? 1.f : 0.f) : x;
-      }
+      for (int e = 0; e < 8; ++e) v[e] = img[po[e] + fo];
       const X3Frag fr = x3_split8(v);
-      char* dst = col + (f * cg.pitch + 8 * g) * 2;
+      char* dst = dstg + f * cg.pitch * 2;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<bf16x8*>(dst + p * partb) = fr.p[p];
+    }
+    // the bias ones column: 1 on the chunk's valid positions, 0 past them
+    if (cg.ones >= 0 && fi == FS - 1) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 8 * g + e < valid_pos ? 1.f : 0.f;
+      const X3Frag fr = x3_split8(v);
+      char* dst = dstg + cg.ones * cg.pitch * 2;
 #pragma unroll
       for (int p = 0; p < 3; ++p) *reinterpret_cast<bf16x8*>(dst + p * partb) = fr.p[p];
     }
   };
-  auto frag = [&](int off, X3Frag& fr) {
+  auto frag = [&](const char* col, int off, X3Frag& fr) {
 #pragma unroll
     for (int p = 0; p < 3; ++p) fr.p[p] = *reinterpret_cast<const bf16x8*>(col + p * partb + off);
   };
-  auto mma = [&](int c) {
-    const int kst = (min(cg.LPC, cg.L - c * cg.LPC) + 15) / 16;  // 16-position k-steps
-    for (int s = 0; s < kst; ++s) {
+  // the fragments of k-step s of every block of the wave (a diagonal block's B is its A)
+  struct KStep {
+    X3Frag A[BPW], B[BPW];
+  };
+  auto load_step = [&](const char* col, int s, KStep& k) {
 #pragma unroll
-      for (int i = 0; i < BPW; ++i) {
-        if (i >= nmine) break;
-        X3Frag A, B;
-        frag(offA[i] + 32 * s, A);
-        if (diag[i]) B = A;
-        else frag(offB[i] + 32 * s, B);
-        x3_six(acc[i], A, B);
-      }
+    for (int i = 0; i < BPW; ++i) {
+      if (i >= nmine) break;
+      frag(col, offA[i] + 32 * s, k.A[i]);
+      if (!diag[i]) frag(col, offB[i] + 32 * s, k.B[i]);
     }
   };
+  auto mul_step = [&](const KStep& k) {
+#pragma unroll
+    for (int i = 0; i < BPW; ++i) {
+      if (i >= nmine) break;
+      x3_six(acc[i], k.A[i], diag[i] ? k.A[i] : k.B[i]);
+    }
+  };
+  // k-steps of chunk c, software-pipelined two deep where the registers allow: step
+  // s + 1's LDS reads are in flight during step s's MFMAs
+  auto mma = [&](const char* col, int c) {
+    const int kst = (min(cg.LPC, cg.L - c * cg.LPC) + 15) / 16;  // 16-position k-steps
+    if constexpr (BPW > 2 || !CX3_PIPE) {  // (two steps of 3 blocks in registers spill)
+      for (int s = kp; s < kst; s += KW) {
+        KStep k;
+        load_step(col, s, k);
+        mul_step(k);
+      }
+      return;
+    }
+    // this wave's k-steps kp + j kw, j < J
+    const int J = kp < kst ? (kst - kp + KW - 1) / KW : 0;
+    if (J == 0) return;
+    KStep k0, k1;
+    load_step(col, kp, k0);
+    int j = 0;
+    for (; j + 2 <= J; j += 2) {
+      load_step(col, kp + (j + 1) * KW, k1);
+      mul_step(k0);
+      if (j + 2 < J) load_step(col, kp + (j + 2) * KW, k0);
+      mul_step(k1);
+    }
+    if (j < J) mul_step(k0);
+  };
 
+  // per image (and chunk of its positions): build the im2col, barrier, multiply,
+  // barrier; the next image's loads fly during the current one and its fp32 copy goes
+  // into the other image buffer (last read by the previous image's builds)
   if (b0 < b1) fetch(b0);
-  __syncthreads();  // (the zero fill before the first commit)
+  __syncthreads();  // (the zero fill and the tables before the first commit)
   if (b0 < b1) commit(0);
   for (int64_t b = b0; b < b1; ++b) {
     const int buf = (int)((b - b0) & 1) * cg.imgf;
     for (int c = 0; c < cg.nch; ++c) {
       __syncthreads();  // image b committed; every wave done reading the previous im2col
-      if (c == 0 && b + 1 < b1) fetch(b + 1);  // next image's loads fly during this one
-      build(buf, c);
+      if (c == 0 && b + 1 < b1) fetch(b + 1);
+      build(colbuf, buf, c);
       __syncthreads();
-      // (the other buffer was last read by the previous image's builds, before the
-      // barrier above)
       if (c == cg.nch - 1 && b + 1 < b1) commit(cg.imgf - buf);
-      mma(c);
+      mma(colbuf, c);
     }
+  }
+  __syncthreads();  // (every wave's last MFMA reads before the partial-sum exchange)
+  // kw > 1: the kw partial sums of a block meet in LDS (the im2col buffers are free
+  // after the last barrier), summed in wave order by its first wave (deterministic)
+  if (KW > 1) {
+    float* red = reinterpret_cast<float*>(colbuf);
+    if (kp > 0 && nmine)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) red[(wave * 16 + v) * 64 + lane] = acc[0][v];
+    __syncthreads();
+    if (kp > 0) return;
+    for (int w = wave + 1; w < wave + KW; ++w)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[0][v] += red[(w * 16 + v) * 64 + lane];
   }
   // block (bi, bj) = quadrant (bi & 1, bj & 1) of slab tile (bi / 2, bj / 2)
 #pragma unroll
   for (int i = 0; i < BPW; ++i) {
     if (i >= nmine) break;
     int bi, bj;
-    tri_decode(wave + CX3_WAVES * i, bi, bj);
+    tri_decode(block_of(i), bi, bj);
     const int ti = bi >> 1, tj = bj >> 1;
     float* o = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.sstride + split) * TILE * TILE +
                (bi & 1) * 32 * TILE + (bj & 1) * 32;
@@ -1992,6 +2065,12 @@ static bool conv_small_off() { return !knobs().conv_small; }
 // Geometry of a conv job on the LDS-staged kernel; false: the job takes the
 // register-staged path (images too large, channel blocks not float4-shaped, or an
 // empty batch).  A multi-batch job's images are its nseg batches' images in order.
+#ifndef CX3_MIN_N
+// smallest factor on mode 4: n in 17..32 (one block, LeNet-5's conv1 A) measured slower
+// here than on the fp32 kernel's three 16x16 blocks (313 vs 139 us per launch, the
+// im2col build of 784 positions per image costs more than the MFMAs save; profiles/r06g/)
+#define CX3_MIN_N 33
+#endif
 // LDS of the mode-4 workgroup: at most 131 KB, so a 29 KB inversion workgroup of an
 // overlapped invert() still fits on the CU (160 KB)
 constexpr int CX3_LDS_MAX = 134144;
@@ -2001,10 +2080,14 @@ constexpr int CX3_LDS_MAX = 134144;
 // image when the whole image does).
 static bool conv_x3_geom(const kfac_operand& o, ConvGeom& g) {
   const int n = g.n;
-  if (n <= 32 || (int64_t)o.C * o.H * o.W > CONV_SRC_MAX || o.sh <= 0 || o.sw <= 0) return false;
+  if (n < CX3_MIN_N || (int64_t)o.C * o.H * o.W > CONV_SRC_MAX || o.sh <= 0 || o.sw <= 0) return false;
   g.nb = (int)cdiv(n, 32);
   g.nq = g.nb * (g.nb + 1) / 2;
-  if (g.nq > 4 * CX3_WAVES) return false;  // (BPW <= 4 blocks per wave)
+  // (at most 3 blocks per wave, n <= 192: 4 need ~300 registers with the build's)
+  if (g.nq > 3 * CX3_WAVES) return false;
+  // one block (17 <= n <= 32: LeNet-5's conv1 A, n = 26 over 784 positions) or three:
+  // its k-steps interleaved over 8 / 2 waves
+  g.kw = g.nq == 1 ? CX3_WAVES : g.nq == 2 ? CX3_WAVES / 2 : g.nq <= 4 ? 2 : 1;
   g.Wp = o.W + 2 * o.pw;
   g.plane = (o.H + 2 * o.ph) * g.Wp;
   g.imgf = o.C * g.plane;
@@ -2022,7 +2105,8 @@ static bool conv_x3_geom(const kfac_operand& o, ConvGeom& g) {
       g.LPC = lpc;
       g.nch = nch;
       g.pitch = pitch;
-      g.ldsb = (int)bytes;
+      // (kw > 1: the epilogue's partial-sum exchange, 8 waves x 16 x 64 floats)
+      g.ldsb = (int)std::max<int64_t>(bytes, g.kw > 1 ? CX3_WAVES * 16 * 64 * 4 : 0);
       g.mode = 4;
       g.units = 1;
       return true;
@@ -2132,8 +2216,7 @@ static void launch_conv(const FactorArgs& args, const ConvGeom& g, int tasks, hi
     const int bpw = (g.nq + CX3_WAVES - 1) / CX3_WAVES;
     const bool ok = bpw <= 1 ? launch_conv_x3<1>(args, g, tasks, stream)
                   : bpw == 2 ? launch_conv_x3<2>(args, g, tasks, stream)
-                  : bpw == 3 ? launch_conv_x3<3>(args, g, tasks, stream)
-                             : launch_conv_x3<4>(args, g, tasks, stream);
+                             : launch_conv_x3<3>(args, g, tasks, stream);
     (void)ok;  // (a failed attribute surfaces as the launch error below)
     return;
   }

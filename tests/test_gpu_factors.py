@@ -137,12 +137,14 @@ def test_conv_golden(hip_device):
     (6, 3, 5, 5, 4, (5, 5), (1, 1), (0, 0), True),
     (2, 3, 40, 40, 5, (3, 3), (1, 1), (1, 1), True),
     (2, 2, 5, 5, 3, (3, 3), (1, 1), (0, 0), True),
-    # kfac_factor_conv_x3 (im2col factors with n > 32, bf16x3 from an LDS im2col): an
-    # image whose 1,024 positions take 4 LDS chunks, stride 2 without bias, and 33 / 224
-    # features (one / seven 32-blocks per edge: 1 / 4 blocks per wave)
+    # kfac_factor_conv_x3 (im2col factors with 32 < n <= 192, bf16x3 from an LDS
+    # im2col): an image whose 1,024 positions take many LDS chunks, stride 2 without
+    # bias, 33 and 181 features (2 / 6 blocks per edge: 1 / 3 blocks per wave, the latter
+    # in 2 chunks of 32 positions), and 224 features (the fp32 kernel again)
     (4, 2, 32, 32, 6, (5, 5), (1, 1), (2, 2), True),
     (5, 4, 15, 15, 8, (3, 3), (2, 2), (1, 1), False),
     (3, 1, 20, 20, 4, (4, 8), (1, 1), (0, 0), True),
+    (2, 20, 10, 10, 5, (3, 3), (1, 1), (0, 0), True),
     (2, 14, 9, 9, 6, (4, 4), (1, 1), (0, 0), False),
 ])
 def test_conv_shapes_vs_oracle(hip_device, spec):
