@@ -11,6 +11,7 @@
 //   2. kfac_factor_reduce: per tile, sum the slabs in split order, apply
 //      F = beta*F + alpha*sum, write the tile and its mirror (LDS transpose),
 //      so F stays exactly symmetric.
+#include <algorithm>
 #include <utility>
 #include <vector>
 #include <type_traits>
@@ -1399,6 +1400,17 @@ struct ConvGeom {
   int ones;        // bias column (-1: none)
   int ldsb;        // bytes of dynamic LDS
   int kw;          // waves per block (nq <= 4: the block's k-steps interleaved over kw waves)
+  // mode 5 (kfac_factor_conv_x3s: one 32 x 32 block from column-shifted image copies)
+  int xs_ncopy;    // copies (C x kernel width), then the ones copy and the zero copy
+  int xs_hp;       // rows per copy (padded image rows)
+  int xs_pw;       // bf16 per copy row (>= 8 xs_g8)
+  int xs_cs;       // bf16 per copy (>= xs_hp xs_pw)
+  int xs_g8;       // 8-position groups per output row (ceil(Wo / 8): 1, 2, 4 or 8)
+  int xs_grp;      // groups per image (Ho xs_g8, even); k-step t holds groups 2t, 2t + 1
+  int xs_np;       // build slots per image (C xs_hp xs_wp2)
+  int xs_wp2;      // build slots per padded row (ceil((W + 2 pw) / 2))
+  int xs_lb[32];   // block row m's fragment byte offset in a part (copy, row, column)
+  int8_t xs_f[32]; // block row m's factor row / column (data, bias, padding rows n..31)
 };
 
 #ifndef KFAC_CONV_OCC
@@ -1975,6 +1987,279 @@ __global__ __launch_bounds__(CX3_THREADS, 1) void kfac_factor_conv_x3(FactorArgs
   }
 }
 
+// ------------------------------- one-block conv factors in bf16x3 (mode 5)
+// The im2col factor of a conv layer with 17 <= n <= 32 (LeNet-5's conv1 A: 26 over 784
+// positions per image, curvatures.py:341-343) as ONE 32 x 32 block, on the bf16 MFMA.
+// An explicit im2col of 784 positions costs more to build than its MFMAs (mode 4 measured
+// 313 vs 139 us for the fp32 mode 3).  Here no im2col is built: the MFMA fragment of
+// feature (c, ki, kj) at output positions (oh, ow0 .. ow0 + 7) is row oh sh + ki,
+// columns ow0 .. ow0 + 7 of a COLUMN COPY (c, kj) of the padded image,
+//   copy(c, kj)[r][ow] = padded[c][r][ow sw + kj]   (0 for ow >= Wo),
+// so the C x kw copies, split once per entry into bf16 hi / mid / lo, hold every
+// fragment as one ds_read_b128 (kh x fewer entries than the im2col).  A k-step is 16
+// positions: lanes 0-31 read group 2t, lanes 32-63 group 2t + 1 (8 positions of one
+// output row each; rows padded to 8 ceil(Wo / 8) positions, the padding zero in every
+// copy).  The bias row reads a ones copy, rows past n a zero copy.  A = B (one diagonal
+// block): six MFMAs per k-step on one fragment triple.
+// One workgroup of 8 waves per CU, two copy buffers, in two groups of 4 waves (one per
+// SIMD each) that swap roles every image: in phase i group i mod 2 multiplies image i
+// (its 4 waves take k-steps wave + 4 j, fragments two k-steps ahead) while the other
+// group builds image i + 1 into the other buffer and then issues the loads of its next
+// image (i + 3: a whole phase to land; buffer loads whose out-of-image offsets return
+// 0); one barrier per phase.  The build splits each image element ONCE and writes it to
+// the kw copies that hold it.  The 8 partial sums meet in LDS in wave order.  The host
+// deals factor rows to block rows so the 16 lanes of each ds_read_b128 group read 16
+// distinct bank quads.
+// Measured on the LeNet-5 pass (conv1 A, 60,000 images; profiles/r06k-r06r): the fp32
+// mode 3 0.685 ms; this kernel 0.47 (MFMA phases alone 0.45, builds alone 0.27).  On
+// the way: one LDS table read per k-step that the fragment addresses waited on, a
+// register mask of odd group counts that waited on the prefetched reads, a conditional
+// prefetch (lgkmcnt(0)), a phase loop whose branch split the in-flight loads' live
+// ranges (vmcnt waits in the MFMA loop), lambdas not inlined (the kernel arguments
+// copied to scratch) and a build that split every copy entry (kw x the VALU) each
+// held it at 0.53-0.69 ms; 8 waves building after their MFMAs 0.67; two 4-wave
+// workgroups per CU with a buffer each 0.67 (their phases stay in step).
+constexpr int XS_THREADS = 512;
+constexpr int XS_WAVES = XS_THREADS / 64;
+constexpr int XS_GROUP = XS_THREADS / 2;  // threads per role group
+constexpr int XS_SP = 4;                  // build slots per group thread and image (<= 1024)
+constexpr int XS_KW = 8;                  // kernel width at most
+constexpr int XS_LDS_MAX = 134144;        // (as mode 4: a 29 KB inversion workgroup still fits beside it)
+constexpr int XS_ZPAD = 256;              // zero bytes after the zero copy: padding rows' column offsets
+constexpr int XS_DUMMY = 16;              // (alignment slack after each part)
+
+// the copy (k) and row offset of block row m (feature m; the bias row; padding rows)
+__host__ __device__ inline void xs_lane(int m, int cols, int ones, int kh, int kw, int ncopy, int& k, int& row) {
+  if (m < cols) {
+    const int kk = kh * kw, c = m / kk, r = m - c * kk, ki = r / kw;
+    k = c * kw + (r - ki * kw);
+    row = ki;
+  } else if (m == ones) {
+    k = ncopy;
+    row = 0;
+  } else {  // (rows < kh: a read stays inside the zero copy)
+    k = ncopy + 1;
+    row = (m - cols) % kh;
+  }
+}
+
+__global__ __launch_bounds__(XS_THREADS, 1) void kfac_factor_conv_x3s(FactorArgs args, ConvGeom cg) {
+  extern __shared__ __attribute__((aligned(16))) char cxs[];
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const int task = xcd_task(blockIdx.x, gridDim.x);
+  int jx = 0;
+  while (jx + 1 < args.njobs && task >= args.task_end[jx]) ++jx;
+  const FactorJobDev& J = args.job[jx];
+  const OpDev& op = J.x;
+  const int split = task - J.task_begin;  // one unit: task = split
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t b0 = (int64_t)split * cg.B / J.splits, b1 = (int64_t)(split + 1) * cg.B / J.splits;
+  // two buffers of [part][copy][row][ow] (copies (c, kj), the ones copy, the zero copy
+  // and its pad)
+  const int partb = (cg.xs_ncopy + 2) * cg.xs_cs * 2 + XS_ZPAD + XS_DUMMY;
+  const int bufb = 3 * partb;
+  // once per task: zero both buffers (padding, out-of-image entries and the zero copy
+  // are never written again), then the ones copies' hi parts
+  for (int e = tid; e < 2 * bufb / 16; e += XS_THREADS)
+    reinterpret_cast<u32x4*>(cxs)[e] = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  // (the rows oh sh the bias row reads)
+  const int Ho = cg.L / cg.Wo;
+  if (cg.ones >= 0)
+    for (int e = tid; e < 2 * Ho * cg.Wo; e += XS_THREADS) {
+      const int bs = e / (Ho * cg.Wo), r = e - bs * Ho * cg.Wo, h = r / cg.Wo;
+      *reinterpret_cast<uint16_t*>(cxs + bs * bufb +
+                                   (cg.xs_ncopy * cg.xs_cs + h * cg.sh * cg.xs_pw + (r - h * cg.Wo)) * 2) = 0x3f80;
+    }
+  // The build, per image element once: thread slot (c, r, col) (col even, padded
+  // coordinates, stride 1) loads elements col .. col + 2 of padded row r of channel c,
+  // splits the pairs (col, col + 1) and (col + 1, col + 2) and writes them to every copy
+  // (c, kj) holding them at an even output column: ow = col - kj (kj even) or
+  // col + 1 - kj (kj odd), when 0 <= ow < Wo (Wo even: a pair is wholly in or out).
+  // Its source byte offsets (outside the image: past the buffer record, loads return
+  // 0), the byte offset of (copy (c, 0), row r, column col) and the mask of kj written.
+  constexpr int OUT = 0x7ffffff0;
+  const int wp2 = cg.xs_wp2, rowp = cg.xs_hp * wp2;
+  int sx[XS_SP][3], dbase[XS_SP], kmask[XS_SP];
+  const int gt = tid % XS_GROUP, grp = wave / (XS_WAVES / 2);  // (both groups build every slot)
+  const int nsp = (cg.xs_np + XS_GROUP - 1) / XS_GROUP;          // slots per thread (uniform)
+#pragma unroll
+  for (int i = 0; i < XS_SP; ++i) {
+    const int e = gt + i * XS_GROUP;
+    sx[i][0] = sx[i][1] = sx[i][2] = OUT;
+    dbase[i] = 0;
+    kmask[i] = 0;
+    if (e < cg.xs_np) {
+      const int c = e / rowp, rem = e - c * rowp, r = rem / wp2, col = 2 * (rem - r * wp2);
+      const int h = r - op.ph;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const int w = col + d - op.pw;
+        if (h >= 0 && h < op.H && w >= 0 && w < op.W) sx[i][d] = ((c * op.H + h) * op.W + w) * 4;
+      }
+      dbase[i] = (c * op.kw * cg.xs_cs + r * cg.xs_pw + col) * 2;
+      for (int kj = 0; kj < op.kw; ++kj) {
+        const int ow = col - kj + (kj & 1);
+        if (ow >= 0 && ow < cg.Wo) kmask[i] |= 1 << kj;
+      }
+    }
+  }
+  const int irec = op.C * op.H * op.W * 4;  // bytes of one image
+  float v0[XS_SP][3];
+  auto fetch = [&](int64_t b) __attribute__((always_inline)) {
+    const int seg = (int)((uint32_t)b / (uint32_t)cg.bseg);
+    const float* src = seg_base(J, args.segs, seg) + (b - (int64_t)seg * cg.bseg) * op.sB;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), 0, irec, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < XS_SP; ++i) {
+      if (i >= nsp) break;
+#pragma unroll
+      for (int d = 0; d < 3; ++d)
+        v0[i][d] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, sx[i][d], 0, 0));
+    }
+  };
+  const int kstep = cg.xs_cs * 2 - 2;  // byte step of (copy kj, column col - kj) per kj
+  auto build = [&](char* buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < XS_SP; ++i) {
+      if (i >= nsp) break;
+      uint32_t p0[3], p1[3];
+      split3(v0[i][0], v0[i][1], p0[0], p0[1], p0[2]);
+      split3(v0[i][1], v0[i][2], p1[0], p1[1], p1[2]);
+#pragma unroll
+      for (int kj = 0; kj < XS_KW; ++kj) {
+        if (kj >= op.kw) break;
+        if (kmask[i] >> kj & 1) {
+          char* d = buf + dbase[i] + kj * kstep + 2 * (kj & 1);
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+            *reinterpret_cast<uint32_t*>(d + q * partb) = (kj & 1) ? p1[q] : p0[q];
+        }
+      }
+    }
+  };
+  // this lane's block row (the host's assignment of factor rows to block rows: lanes
+  // of one ds_read_b128 group on distinct bank quads); lanes 32-63 take the odd groups
+  // (tables read with constant indices only: a lane-indexed read of the by-value
+  // argument copies the kernel arguments to scratch and reloads fields from there)
+  const int hi = lane >> 5;
+  int lbase = 0, fme = 0;
+#pragma unroll
+  for (int t = 0; t < 32; ++t) {
+    int e = cg.xs_lb[t], f = cg.xs_f[t];
+    asm volatile("" : "+s"(e), "+s"(f));  // (opaque: no select of addresses)
+    lbase = (lane & 31) == t ? e : lbase;
+    fme = tid == t ? f : fme;
+  }
+  __shared__ int ftab[32];  // block row -> factor row / column (the epilogue's stores)
+  if (tid < 32) ftab[tid] = fme;
+  floatx16 acc;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+  // group q = 2t + hi of k-step t: output row q / g8, columns 8 (q mod g8) .. + 7.  A
+  // wave's k-steps t = gw + 4 j are groups q0 + 8 j, and g8 divides 8, so its fragment
+  // addresses are a0 + j delta (no per-k-step index math; a table read in LDS, which the
+  // addresses waited on, put its latency in front of every k-step's MFMAs).  The group
+  // count is even (host), so every k-step holds two real groups.
+  constexpr int GW = XS_WAVES / 2;
+  const int nks = cg.xs_grp / 2, gw = wave % GW;
+  const int Jn = gw < nks ? (nks - gw + GW - 1) / GW : 0;
+  const int q0 = 2 * gw + hi, oh0 = q0 / cg.xs_g8;
+  const int a0 = lbase + oh0 * cg.sh * cg.xs_pw * 2 + 16 * (q0 - oh0 * cg.xs_g8);
+  const int delta = (8 / cg.xs_g8) * cg.sh * cg.xs_pw * 2;
+  auto load = [&](const char* buf, int j, X3Frag& fr) __attribute__((always_inline)) {
+    const char* p = buf + a0 + j * delta;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) fr.p[r] = *reinterpret_cast<const bf16x8*>(p + r * partb);
+  };
+  // this wave's k-steps of an image (gw: its index in the group), the next one's reads
+  // in flight during the current one's MFMAs
+  auto mma = [&](const char* buf) __attribute__((always_inline)) {
+    if (Jn == 0) return;
+    // (scheduling fences: left alone the compiler sinks each prefetch behind the MFMAs
+    // of the fragments whose registers it reuses, and every k-step waits for its reads;
+    // the loads are unconditional -- past the last k-step a harmless reload -- since a
+    // conditional load made the next wait lgkmcnt(0))
+    const int last = Jn - 1;
+    X3Frag k0, k1, k2;
+    load(buf, 0, k0);
+    load(buf, min(1, last), k1);
+    int j = 0;
+    for (; j + 3 <= Jn; j += 3) {
+      load(buf, min(j + 2, last), k2);
+      __builtin_amdgcn_sched_barrier(0);
+      x3_six(acc, k0, k0);
+      __builtin_amdgcn_sched_barrier(0);
+      load(buf, min(j + 3, last), k0);
+      __builtin_amdgcn_sched_barrier(0);
+      x3_six(acc, k1, k1);
+      __builtin_amdgcn_sched_barrier(0);
+      load(buf, min(j + 4, last), k1);
+      __builtin_amdgcn_sched_barrier(0);
+      x3_six(acc, k2, k2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (j < Jn) x3_six(acc, k0, k0);
+    if (j + 1 < Jn) x3_six(acc, k1, k1);
+  };
+
+  // phase i: group i % 2 multiplies image i, the other group builds image i + 1, then
+  // loads image i + 3 (its next build); group 0 builds image 0 first.  One code path per
+  // group, each phase pair straight-line: with one loop and a branch per phase the
+  // compiler gave the in-flight loads the fragment registers (live ranges split at the
+  // branch), and loads in flight on any path into a loop head (the other group's
+  // prologue, this group's own) made it wait on them inside every multiply phase
+  const int64_t nimg = b1 - b0;
+  auto phase_mma = [&](int64_t i) __attribute__((always_inline)) {
+    if (i < nimg) mma(cxs + (int)(i & 1) * bufb);
+    __syncthreads();
+  };
+  auto phase_build = [&](int64_t i) __attribute__((always_inline)) {
+    if (i + 1 < nimg) {
+      build(cxs + (int)((i + 1) & 1) * bufb);
+      if (i + 3 < nimg) fetch(b0 + i + 3);
+    }
+    __syncthreads();
+  };
+  if (grp == 0) {
+    if (nimg > 0) {
+      fetch(b0);
+      build(cxs);
+      if (nimg > 2) {
+        fetch(b0 + 2);
+#pragma unroll
+        for (int i = 0; i < XS_SP; ++i) asm volatile("" ::"v"(v0[i][0]), "v"(v0[i][1]), "v"(v0[i][2]));  // (landed)
+      }
+    }
+    __syncthreads();
+    for (int64_t i = 0; i < nimg; i += 2) {
+      phase_mma(i);
+      phase_build(i + 1);
+    }
+  } else {
+    if (nimg > 1) fetch(b0 + 1);
+    __syncthreads();
+    for (int64_t i = 0; i < nimg; i += 2) {
+      phase_build(i);
+      phase_mma(i + 1);
+    }
+  }
+  // the 8 waves' partial sums, summed in wave order by wave 0 (deterministic)
+  float* red = reinterpret_cast<float*>(cxs);
+  if (wave > 0)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) red[((wave - 1) * 16 + v) * 64 + lane] = acc[v];
+  __syncthreads();
+  if (wave > 0) return;
+  for (int w = 0; w < XS_WAVES - 1; ++w)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[v] += red[(w * 16 + v) * 64 + lane];
+  float* o = J.slab + (size_t)split * TILE * TILE;  // block (0, 0) of slab tile 0
+  const int fc = ftab[lane & 31];
+  put_partial(J, acc, [&](int v) { return &o[ftab[acc_row(v, lane)] * TILE + fc]; });
+}
+
 // Channel-major factors with n <= 8 (the G of a conv layer with few output
 // channels, e.g. LeNet-5's conv1: 6): F = sum over (image, position) of g g^T is
 // n(n+1)/2 FMAs per position against n loads -- an HBM stream, not MFMA work.  Each
@@ -2068,7 +2353,8 @@ static bool conv_small_off() { return !knobs().conv_small; }
 #ifndef CX3_MIN_N
 // smallest factor on mode 4: n in 17..32 (one block, LeNet-5's conv1 A) measured slower
 // here than on the fp32 kernel's three 16x16 blocks (313 vs 139 us per launch, the
-// im2col build of 784 positions per image costs more than the MFMAs save; profiles/r06g/)
+// im2col build of 784 positions per image costs more than the MFMAs save; profiles/r06g/);
+// those factors take mode 5 (column copies, no im2col) where its geometry fits
 #define CX3_MIN_N 33
 #endif
 // LDS of the mode-4 workgroup: at most 131 KB, so a 29 KB inversion workgroup of an
@@ -2115,6 +2401,112 @@ static bool conv_x3_geom(const kfac_operand& o, ConvGeom& g) {
   return false;
 }
 
+// Mode 5 (kfac_factor_conv_x3s): an im2col operand with 17 <= n <= 32 whose column
+// copies fit XS_LDS_MAX and take at most XS_SP build slots per thread.  The
+// copy row pitch and copy stride (multiples of 8 bf16) are searched for the fewest lanes
+// of a 16-lane group on one 16-byte bank quad (their fragment reads differ by the copy
+// and row offsets of xs_lane; the group offset is uniform), then the fewest bytes.
+// the ds_read_b128 lane group (of lanes 0-31; 32-63 repeat it) of lane m:
+// {0-3, 12-15, 20-27} and {4-11, 16-19, 28-31} (MI355X_MICROARCH.md, LDS)
+static inline int b128_group(int m) { return (m >= 4 && m < 12) || (m >= 16 && m < 20) || m >= 28; }
+
+static bool conv_x3s_geom(const kfac_operand& o, ConvGeom& g) {
+  const int n = g.n;
+  // (the build's pair slots: column stride 1, even Wo, kernel width <= XS_KW)
+  if (n < 17 || n > 32 || o.sh <= 0 || o.sw != 1 || o.Ho <= 0 || o.Wo <= 0 || o.Wo % 2 != 0 ||
+      o.kw > XS_KW)
+    return false;
+  const int hp = o.H + 2 * o.ph, g8 = (int)cdiv(o.Wo, 8), ncopy = o.C * o.kw;
+  // (a wave's k-steps advance by whole output rows; every k-step two real groups)
+  if (8 % g8 != 0 || o.Ho * g8 % 2 != 0) return false;
+  const int wp2 = (o.W + 2 * o.pw + 1) / 2;
+  const int64_t np = (int64_t)o.C * hp * wp2;
+  if (np > (int64_t)XS_SP * XS_GROUP) return false;
+  const int grp = o.Ho * g8, ones = o.has_ones ? o.cols : -1;
+  // the data and bias rows' fragment offsets at row pitch pw, copy stride cs; their
+  // 16-byte bank quads (a ds_read_b128 group of 16 lanes is conflict-free on 16
+  // distinct quads); padding rows read the zero copy at any of 16 column offsets
+  struct Item { int quad, lb, f; };
+  auto items_of = [&](int64_t pw, int64_t cs, std::vector<Item>& it) {
+    it.clear();
+    for (int f = 0; f < o.cols + (ones >= 0 ? 1 : 0); ++f) {
+      int k, row;
+      xs_lane(f, o.cols, ones, o.kh, o.kw, ncopy, k, row);
+      const int64_t lb = (k * cs + row * pw) * 2;
+      it.push_back({(int)((lb / 16) % 16), (int)lb, f});
+    }
+  };
+  int best_w = 1 << 30;
+  int64_t best_b = 0;
+  std::vector<Item> it;
+  for (int pw = 8 * g8; pw < 8 * g8 + 128; pw += 8)
+    for (int s = 0; s < 16; ++s) {
+      int64_t cs = (int64_t)hp * pw;
+      while ((cs / 8) % 16 != s) cs += 8;
+      const int64_t bytes = (int64_t)2 * 3 * ((ncopy + 2) * cs * 2 + XS_ZPAD + XS_DUMMY);
+      if (bytes > XS_LDS_MAX) continue;
+      items_of(pw, cs, it);
+      int cnt[16] = {0}, worst = 0;
+      for (const Item& x : it) worst = std::max(worst, ++cnt[x.quad]);
+      worst = (worst + 1) / 2;  // (split over the two lane groups)
+      if (worst < best_w || (worst == best_w && bytes < best_b)) {
+        best_w = worst;
+        best_b = bytes;
+        g.xs_pw = pw;
+        g.xs_cs = (int)cs;
+      }
+    }
+  if (best_w == 1 << 30) return false;
+  // deal the rows to the two lane groups, each quad's users alternately, then pad each
+  // group to 16 lanes with zero-copy reads on the quads it has least
+  items_of(g.xs_pw, g.xs_cs, it);
+  std::sort(it.begin(), it.end(), [](const Item& a, const Item& b) { return a.quad < b.quad; });
+  std::vector<Item> grpl[2];
+  int use[2][16] = {{0}};
+  for (const Item& x : it) {
+    int q = use[0][x.quad] < use[1][x.quad] ? 0 : use[1][x.quad] < use[0][x.quad] ? 1
+            : grpl[0].size() <= grpl[1].size() ? 0 : 1;
+    if (grpl[q].size() == 16) q = 1 - q;
+    grpl[q].push_back(x);
+    ++use[q][x.quad];
+  }
+  const int64_t zb = (int64_t)(ncopy + 1) * g.xs_cs * 2;
+  int fpad = n;
+  for (int q = 0; q < 2; ++q)
+    while (grpl[q].size() < 16) {
+      int quad = 0;
+      for (int t = 1; t < 16; ++t)
+        if (use[q][t] < use[q][quad]) quad = t;
+      const int col = (int)(((quad - (zb / 16) % 16) % 16 + 16) % 16);
+      grpl[q].push_back({quad, (int)(zb + 16 * col), fpad++});
+      ++use[q][quad];
+    }
+  for (int m = 0, c[2] = {0, 0}; m < 32; ++m) {
+    const int q = b128_group(m);
+    const Item& x = grpl[q][c[q]++];
+    g.xs_lb[m] = x.lb;
+    g.xs_f[m] = (int8_t)x.f;
+  }
+  g.xs_ncopy = ncopy;
+  g.xs_hp = hp;
+  g.xs_g8 = g8;
+  g.xs_grp = grp;
+  g.xs_np = (int)np;
+  g.xs_wp2 = wp2;
+  g.L = (int)o.L;
+  g.Wo = o.Wo;
+  g.sh = o.sh;
+  g.sw = o.sw;
+  g.ones = ones;
+  // (the epilogue's partial-sum exchange: 7 waves x 16 x 64 floats)
+  g.ldsb = (int)std::max<int64_t>(best_b, (XS_WAVES - 1) * 16 * 64 * 4);
+  g.nb = 1;
+  g.nq = 1;
+  g.mode = 5;
+  g.units = 1;
+  return true;
+}
+
 static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
   const kfac_operand& o = j.x;
   const int64_t nseg = j.nseg > 1 ? j.nseg : 1;
@@ -2126,7 +2518,7 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
   g.n = n;
   g.bseg = (int)(o.rows / o.L);
   g.B = (int)(nseg * g.bseg);
-  if (o.layout == KFAC_PATCH && knobs().conv_x3 && conv_x3_geom(o, g)) return true;
+  if (o.layout == KFAC_PATCH && knobs().conv_x3 && (conv_x3s_geom(o, g) || conv_x3_geom(o, g))) return true;
 #ifndef KFAC_CONV_NARROW32
 #define KFAC_CONV_NARROW32 3  // n in 17..32: 3 = three 16x16 blocks, 1 = one 32x32 block (A/B)
 #endif
@@ -2212,6 +2604,14 @@ static bool launch_conv_x3(const FactorArgs& args, const ConvGeom& g, int tasks,
 
 template <int LAYOUT>
 static void launch_conv(const FactorArgs& args, const ConvGeom& g, int tasks, hipStream_t stream) {
+  if (g.mode == 5) {
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&kfac_factor_conv_x3s),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 XS_LDS_MAX) == hipSuccess;
+    (void)attr;  // (a failed attribute surfaces as the launch error)
+    hipLaunchKernelGGL(kfac_factor_conv_x3s, dim3(tasks), dim3(XS_THREADS), (size_t)g.ldsb, stream, args, g);
+    return;
+  }
   if (g.mode == 4) {
     const int bpw = (g.nq + CX3_WAVES - 1) / CX3_WAVES;
     const bool ok = bpw <= 1 ? launch_conv_x3<1>(args, g, tasks, stream)
@@ -2535,8 +2935,8 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
       // larger cost there: conv1 G 15.7 / 12.4 / 13.2 us at k = 1 / 2 / 4)
       const bool small = jobs[i].x.layout == KFAC_CHANNEL && cg.n <= 8 && !conv_small_off();
       // (mode-0 instances are compiled for KFAC_CONV_OCC resident workgroups per CU;
-      // mode 4 runs one 512-thread workgroup per CU)
-      const int64_t cslots = cg.mode == 0 ? (int64_t)KFAC_CONV_OCC * 256 : cg.mode == 4 ? 256 : slots;
+      // modes 4 and 5 run one 512-thread workgroup per CU)
+      const int64_t cslots = cg.mode == 0 ? (int64_t)KFAC_CONV_OCC * 256 : cg.mode >= 4 ? 256 : slots;
       int k = (int)std::max<int64_t>(1, cdiv((int64_t)cg.units * cg.B, small ? cslots / 2 : cslots));
       if (knobs().conv_k > 0) k = knobs().conv_k;
       k = std::min(k, cg.B);
@@ -2681,6 +3081,7 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
                      : !staged ? KFAC_PROF_FACTOR_TILES
                      : (jobs[0].x.layout == KFAC_CHANNEL && cg.n <= 8 && !conv_small_off())
                          ? KFAC_PROF_FACTOR_CHANNEL_SMALL
+                     : cg.mode == 5 ? KFAC_PROF_FACTOR_CONV_X3S
                      : cg.mode == 4 ? KFAC_PROF_FACTOR_CONV_X3 : KFAC_PROF_FACTOR_CONV;
     double work = 0.0, bytes = 0.0;
     if (prof_on())

@@ -120,6 +120,11 @@ def test_conv_golden(hip_device):
         np.testing.assert_allclose(G.cpu().numpy(), g[f"G{li}"], **FT)
 
 
+X3S_SPECS = [(16, 1, 28, 28, 6, (5, 5), (1, 1), (2, 2), True), (256, 1, 28, 28, 6, (5, 5), (1, 1), (2, 2), True),
+             (5, 2, 11, 13, 4, (3, 4), (2, 1), (1, 2), True),
+             (3, 3, 12, 16, 5, (3, 3), (1, 1), (0, 1), False), (2, 2, 9, 9, 3, (4, 4), (1, 1), (1, 1), False)]
+
+
 @pytest.mark.parametrize("spec", [
     # (B, Cin, H, W, Cout, k, stride, pad, bias): LeNet-5 / BaseNet_15k shapes + odd ones
     (16, 1, 28, 28, 6, (5, 5), (1, 1), (2, 2), True),
@@ -146,8 +151,18 @@ def test_conv_golden(hip_device):
     (3, 1, 20, 20, 4, (4, 8), (1, 1), (0, 0), True),
     (2, 20, 10, 10, 5, (3, 3), (1, 1), (0, 0), True),
     (2, 14, 9, 9, 6, (4, 4), (1, 1), (0, 0), False),
+    # kfac_factor_conv_x3s (im2col factors with 17 <= n <= 32, bf16x3 from column-
+    # shifted image copies; LeNet-5's conv1 above; 19 features over 3 groups above: an
+    # odd group count, which stays on the fp32 kernel): row stride 2 with asymmetric
+    # padding and 14 output columns (two groups per row, the second 6 wide), 27
+    # features without bias over 16 columns (column stride 3: the fp32 kernel), n = 32
+    (5, 2, 11, 13, 4, (3, 4), (2, 1), (1, 2), True),
+    (3, 3, 12, 16, 5, (3, 3), (1, 1), (0, 1), False),
+    (3, 3, 12, 17, 5, (3, 3), (1, 3), (0, 1), False),
+    (2, 2, 9, 9, 3, (4, 4), (1, 1), (1, 1), False),
 ])
 def test_conv_shapes_vs_oracle(hip_device, spec):
+    from bnn_kfac_amd import _native as N
     from bnn_kfac_amd.curvatures import KFAC
     B, Cin, H, W, Cout, k, s, p, bias = spec
     rng = np.random.default_rng(sum(spec[:5]))
@@ -157,7 +172,13 @@ def test_conv_shapes_vs_oracle(hip_device, spec):
     gr = rng.standard_normal((B, Cout, Ho, Wo), dtype=np.float32)
     kfac = KFAC(conv)
     kfac.record[conv] = [_t(x, hip_device), _t(gr, hip_device)]
+    N.profile_reset()
+    N.profile_enable(True)
     kfac.update(batch_size=B)
+    torch.cuda.synchronize()
+    N.profile_enable(False)
+    if spec in X3S_SPECS:  # the A factor on the column-copy kernel, one launch
+        assert N.profile_read(N.PROF_FACTOR_CONV_X3S)[1] == 1
     A, G = kfac.state[conv]
     np.testing.assert_allclose(A.cpu().numpy(), O.conv_factor_A(x, k, p, s, bias, np.float64), **FT)
     np.testing.assert_allclose(G.cpu().numpy(), O.grad_factor(gr, np.float64), **FT)
