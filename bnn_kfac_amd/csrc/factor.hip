@@ -1893,32 +1893,33 @@ __global__ __launch_bounds__(CX3_THREADS, 1) void kfac_factor_conv_x3(FactorArgs
       for (int p = 0; p < 3; ++p) *reinterpret_cast<bf16x8*>(dst + p * partb) = fr.p[p];
     }
   };
-  auto frag = [&](const char* col, int off, X3Frag& fr) {
+  auto frag = [&](const char* col, int off, X3Frag& fr) __attribute__((always_inline)) {
 #pragma unroll
     for (int p = 0; p < 3; ++p) fr.p[p] = *reinterpret_cast<const bf16x8*>(col + p * partb + off);
   };
-  // the fragments of k-step s of every block of the wave (a diagonal block's B is its A)
+  // the fragments of k-step s of every block slot of the wave, unconditionally: a
+  // diagonal block reads its A twice, a slot past the wave's blocks block (0, 0), and its
+  // MFMAs go to an accumulator never stored (a conditional read made the compiler wait
+  // lgkmcnt(0) in front of every block's MFMAs)
   struct KStep {
     X3Frag A[BPW], B[BPW];
   };
-  auto load_step = [&](const char* col, int s, KStep& k) {
+  auto load_step = [&](const char* col, int s, KStep& k) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < BPW; ++i) {
-      if (i >= nmine) break;
       frag(col, offA[i] + 32 * s, k.A[i]);
-      if (!diag[i]) frag(col, offB[i] + 32 * s, k.B[i]);
+      frag(col, offB[i] + 32 * s, k.B[i]);
     }
   };
-  auto mul_step = [&](const KStep& k) {
+  auto mul_step = [&](const KStep& k) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < BPW; ++i) {
-      if (i >= nmine) break;
-      x3_six(acc[i], k.A[i], diag[i] ? k.A[i] : k.B[i]);
-    }
+    for (int i = 0; i < BPW; ++i) x3_six(acc[i], k.A[i], k.B[i]);
   };
   // k-steps of chunk c, software-pipelined two deep where the registers allow: step
-  // s + 1's LDS reads are in flight during step s's MFMAs
-  auto mma = [&](const char* col, int c) {
+  // s + 1's LDS reads are in flight during step s's MFMAs (scheduling fences: left alone
+  // the compiler sinks the prefetch behind the MFMAs; past the last k-step the prefetch
+  // reloads it, unconditionally)
+  auto mma = [&](const char* col, int c) __attribute__((always_inline)) {
     const int kst = (min(cg.LPC, cg.L - c * cg.LPC) + 15) / 16;  // 16-position k-steps
     if constexpr (BPW > 2 || !CX3_PIPE) {  // (two steps of 3 blocks in registers spill)
       for (int s = kp; s < kst; s += KW) {
@@ -1936,9 +1937,13 @@ __global__ __launch_bounds__(CX3_THREADS, 1) void kfac_factor_conv_x3(FactorArgs
     int j = 0;
     for (; j + 2 <= J; j += 2) {
       load_step(col, kp + (j + 1) * KW, k1);
+      __builtin_amdgcn_sched_barrier(0);
       mul_step(k0);
-      if (j + 2 < J) load_step(col, kp + (j + 2) * KW, k0);
+      __builtin_amdgcn_sched_barrier(0);
+      load_step(col, kp + min(j + 2, J - 1) * KW, k0);
+      __builtin_amdgcn_sched_barrier(0);
       mul_step(k1);
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (j < J) mul_step(k0);
   };
