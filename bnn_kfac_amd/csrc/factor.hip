@@ -508,8 +508,9 @@ __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs ar
 // back by LDS-DMA.
 // LDS image of a substep: [part][column][2 chunks of 8 k] (32 B per column, k
 // contiguous), read straight into MFMA operands (lane = column, 8 k per
-// ds_read_b128); the chunk of a column is XOR-swizzled by bit 3 of the column, so the
-// fragment reads are conflict-free and each is a per-lane base plus an immediate.
+// ds_read_b128); the chunk of a column is XOR-swizzled (s3_half), so the fragment
+// reads and the split's writes are conflict-free and each read is a per-lane base plus
+// an immediate.
 // (A first version split in 8 producer waves beside 4 consumer waves per workgroup:
 // producer-bound at 0.25 of the roofline)
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -517,8 +518,12 @@ constexpr int MT = 128;                          // macro tile edge
 constexpr int S3_PART = 2 * MT * 32;             // bytes of one part of a substep slot (A and B)
 constexpr int S3_REG = 3 * S3_PART + 64;         // one substep slot (+64: bank offset)
 
-// byte offset of half-chunk hh (k 8hh .. 8hh+7 of a substep) of column c in a part
-__device__ __forceinline__ int s3_half(int c, int hh) { return c * 32 + ((hh ^ ((c >> 3) & 1)) << 4); }
+// byte offset of half-chunk hh (k 8hh .. 8hh+7 of a substep) of column c in a part.
+// The half is swapped by bit 2 ^ bit 3 of the column: the fragment reads (ds_read_b128,
+// lane groups {0-3, 12-15, 20-27} / {4-11, 16-19, 28-31}) and the split's writes
+// (ds_write_b128, 8 consecutive columns) both hit distinct bank quads (bit 3 alone left
+// the writes 2-way conflicted: 2.7 conflict cycles per LDS instruction, profiles/r06a_wide/)
+__device__ __forceinline__ int s3_half(int c, int hh) { return c * 32 + ((hh ^ (((c >> 2) ^ (c >> 3)) & 1)) << 4); }
 
 // (a, b) -> bf16 pair (a low), round to nearest even.  Inline asm: from a plain
 // cast the compiler re-derives (pair << 16) as a second conversion of (a, 0)
