@@ -451,10 +451,7 @@ __device__ __forceinline__ void factor_task_glds(const FactorJobDev& J, const fl
 // workgroups that share a CU start ~1 us apart, so their load / barrier stalls
 // interleave instead of coinciding (fp32 LDS-DMA SYRK: +2.5 %).  A design
 // constant, not a timing build.
-#ifndef KFAC_STAGGER
-#define KFAC_STAGGER 5
-#endif
-constexpr int STAGGER = KFAC_STAGGER;
+constexpr int STAGGER = 5;
 
 template <int GBK, int NSLOT, bool GLDS_ONLY = false, int FAMILY = KFAC_ROWMAJOR>
 __global__ __launch_bounds__(NTHREADS, 4) void kfac_factor_tiles_t(FactorArgs args) {
@@ -628,9 +625,7 @@ __device__ __forceinline__ void s3_decode(int unit, int T3, int& I, int& J) {
 // as 2 x 2 blocks, six products per block: 24 MFMAs per substep against 2 columns x
 // 16 values split per thread (3.7 VALU per MFMA; tools/microbench/cutq_mb.hip: 0.448
 // of 417 TF/s on a 4096-column operand).
-#ifndef KFAC_S3D_WGS
-#define KFAC_S3D_WGS 2  // resident workgroups per CU the planner counts on
-#endif
+constexpr int KFAC_S3D_WGS = 2;  // resident workgroups per CU the planner counts on
 constexpr int S3D_WGS = KFAC_S3D_WGS;
 constexpr int S3D_LDS = 2 * S3_REG;
 
@@ -1371,9 +1366,7 @@ constexpr int CONV_CB = 2;  // 32x32 blocks per wave (mode 0): 4*CONV_CB per wor
 // LDS latency) instead of 4 keeps the PATCH instances inside the 128-VGPR budget of 4
 // workgroups per CU without spilling (LeNet-5: conv 2.90 vs 3.04 ms per pass, 1.69 vs
 // 1.63e7 img/s, 3 alternating runs, profiles/r06b/)
-#ifndef CONV_CK2
-#define CONV_CK2 2
-#endif
+constexpr int CONV_CK2 = 2;
 
 struct ConvGeom {
   int mode;        // 0: 64x64 tiles, 1: narrow 32x32, 2: narrow 16x16
@@ -1418,9 +1411,7 @@ struct ConvGeom {
   int8_t xs_f[32]; // block row m's factor row / column (data, bias, padding rows n..31)
 };
 
-#ifndef KFAC_CONV_OCC
-#define KFAC_CONV_OCC 4  // resident workgroups per CU the mode-0 instances are compiled for
-#endif
+constexpr int KFAC_CONV_OCC = 4;  // resident workgroups per CU the mode-0 instances are compiled for
 template <int LAYOUT, int PMAXE, bool STRIDE1, int CB = CONV_CB, bool M3 = false>
 __global__ __launch_bounds__(NTHREADS, (CB == 2 && !M3) ? KFAC_CONV_OCC : 4) void kfac_factor_conv(
     FactorArgs args, ConvGeom cg) {
@@ -1764,9 +1755,7 @@ __global__ __launch_bounds__(NTHREADS, (CB == 2 && !M3) ? KFAC_CONV_OCC : 4) voi
 // 0-3 building while waves 4-7 multiply (and the other way round): 389 vs 306 us per
 // launch -- the 48-position chunks cost more per-chunk overhead than the overlap saved
 // (profiles/r06g/).  Partials go to the slab tiles of the other conv paths.
-#ifndef CX3_PIPE
-#define CX3_PIPE 1
-#endif
+constexpr bool CX3_PIPE = 1;
 constexpr int CX3_THREADS = 512;
 constexpr int CX3_WAVES = CX3_THREADS / 64;
 constexpr int CX3_PM = CONV_SRC_MAX / CX3_THREADS;  // staged source elements per thread
@@ -2360,13 +2349,11 @@ static bool conv_small_off() { return !knobs().conv_small; }
 // Geometry of a conv job on the LDS-staged kernel; false: the job takes the
 // register-staged path (images too large, channel blocks not float4-shaped, or an
 // empty batch).  A multi-batch job's images are its nseg batches' images in order.
-#ifndef CX3_MIN_N
 // smallest factor on mode 4: n in 17..32 (one block, LeNet-5's conv1 A) measured slower
 // here than on the fp32 kernel's three 16x16 blocks (313 vs 139 us per launch, the
 // im2col build of 784 positions per image costs more than the MFMAs save; profiles/r06g/);
 // those factors take mode 5 (column copies, no im2col) where its geometry fits
-#define CX3_MIN_N 33
-#endif
+constexpr int CX3_MIN_N = 33;
 // LDS of the mode-4 workgroup: at most 131 KB, so a 29 KB inversion workgroup of an
 // overlapped invert() still fits on the CU (160 KB)
 constexpr int CX3_LDS_MAX = 134144;
@@ -2529,9 +2516,7 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
   g.bseg = (int)(o.rows / o.L);
   g.B = (int)(nseg * g.bseg);
   if (o.layout == KFAC_PATCH && knobs().conv_x3 && (conv_x3s_geom(o, g) || conv_x3_geom(o, g))) return true;
-#ifndef KFAC_CONV_NARROW32
-#define KFAC_CONV_NARROW32 3  // n in 17..32: 3 = three 16x16 blocks, 1 = one 32x32 block (A/B)
-#endif
+constexpr int KFAC_CONV_NARROW32 = 3;  // n in 17..32: 3 = three 16x16 blocks, 1 = one 32x32 block (A/B)
   g.mode = n <= 16 ? 2 : (n <= 32 ? KFAC_CONV_NARROW32 : 0);
   g.KR = g.mode >= 2 ? 4 : 2;
   int64_t lds;
