@@ -12,6 +12,7 @@
 //      F = beta*F + alpha*sum, write the tile and its mirror (LDS transpose),
 //      so F stays exactly symmetric.
 #include <algorithm>
+#include <initializer_list>
 #include <utility>
 #include <vector>
 #include <type_traits>
@@ -1407,6 +1408,14 @@ struct ConvGeom {
   int xs_grp;      // groups per image (Ho xs_g8, even); k-step t holds groups 2t, 2t + 1
   int xs_np;       // build slots per image (C xs_hp xs_wp2)
   int xs_wp2;      // build slots per padded row (ceil((W + 2 pw) / 2))
+  // mode 6 (kfac_factor_conv_x3f: flattened column copies; xs_hp / xs_wp2 / xs_np too)
+  int xf_ncp;      // copies: C x kw x xf_nv (then the ones copy and the zero copy)
+  int xf_cl;       // bf16 per copy (Hp Wo + 20, multiple of 8)
+  int xf_nv;       // shifted variants per copy (8-byte fragment reads)
+  int xf_smap;     // variant v's shift (elements) in bits 2v .. 2v+1
+  int xf_vmap;     // kernel row ki's variant in bits 2ki .. 2ki+1
+  int xf_nks;      // 16-position k-steps per image (ceil(L / 16))
+  int xf_wave[4];  // multiplying wave w: pattern (bits 0-3) and F[q] (bits 4 + 3q ..)
   int xs_lb[32];   // block row m's fragment byte offset in a part (copy, row, column)
   int8_t xs_f[32]; // block row m's factor row / column (data, bias, padding rows n..31)
 };
@@ -2259,6 +2268,325 @@ __global__ __launch_bounds__(XS_THREADS, 1) void kfac_factor_conv_x3s(FactorArgs
   put_partial(J, acc, [&](int v) { return &o[ftab[acc_row(v, lane)] * TILE + fc]; });
 }
 
+// ------------------------- conv factors from flattened column copies (mode 6)
+// The im2col factor of a stride-1 conv layer with 32 < n <= 160 (LeNet-5's conv2 A: 151
+// features over 100 positions per image, curvatures.py:341-343) without an im2col.
+// With the output positions flattened, p = oh Wo + ow, the patch entry of feature
+// (c, ki, kj) at p is padded[c][oh + ki][ow + kj] = copy(c, kj)[ki Wo + p], where
+//   copy(c, kj)[r Wo + ow] = padded[c][r][ow + kj]      (r < Hp, ow < Wo)
+// is the padded image's column window of width Wo, rows kept at pitch Wo.  So C x kw
+// copies (kh x fewer entries than the im2col, 25 KB per LeNet-5 image in three bf16
+// parts instead of 102 KB) hold every MFMA fragment -- 8 consecutive positions of one
+// feature -- at element ki Wo + p.  8-byte reads need ki Wo + shift = 0 mod 4: each copy
+// is kept in NV <= 4 variants shifted by the residues the kernel rows need (LeNet-5
+// conv2, Wo = 10: shifts 0 and 2).  Positions past L in the last 16-position k-step
+// read the next rows' data, so that k-step's A fragments are masked.  The bias row
+// reads a ones copy, padding rows a zero copy.
+// As in mode 5: one workgroup of 8 waves per CU, two copy buffers, two groups of 4
+// waves that swap roles every image (one multiplies image i, the other builds image
+// i + 1 and loads image i + 3); a multiplying wave takes blocks gw + 4 j of the lower
+// triangle (<= 4) over every k-step, the next (k-step, block) unit's fragments in
+// flight during the current one's MFMAs.  The build splits each image element once and
+// writes it (as bf16 pairs) to the kw NV copy slots that hold it.  At the end the two
+// groups' partial sums of a block meet in LDS (group 1's added to group 0's).
+constexpr int XF_THREADS = 512;
+constexpr int XF_WAVES = XF_THREADS / 64;
+constexpr int XF_GROUP = XF_THREADS / 2;  // threads per role group
+constexpr int XF_GW = XF_WAVES / 2;       // waves per role group
+constexpr int XF_SP = 3;                  // build slots per group thread and image (<= 768)
+constexpr int XF_BPW = 4;                 // blocks per multiplying wave (nq <= 16)
+constexpr int XF_KW = 8;                  // kernel width at most
+constexpr int XF_LDS_MAX = 134144;        // (a 29 KB inversion workgroup still fits beside it)
+
+// A multiplying wave's blocks as pairs (a, b) of indices into its fragment set F: block
+// (F[a], F[b]).  Assignments (conv_x3f_geom): 5 block rows (n = 129..160): waves take
+// patterns 0-3 with F = {0,1,4}, {0,1,2,3}, {0,1,2,4}, {2,3,4}; 4 block rows (97..128):
+// patterns 4-6 with F = {0,1}, {0,1,2}, {0,1,2,3} and an idle wave.
+struct XfPat {
+  int a[4], b[4], n;
+};
+constexpr XfPat XF_PAT[] = {
+    {{0, 1, 1, 2}, {0, 0, 1, 2}, 4}, {{2, 2, 3, 3}, {0, 1, 0, 1}, 4}, {{3, 3, 3, 2}, {0, 1, 2, 2}, 4},
+    {{1, 1, 2, 0}, {0, 1, 1, 0}, 3}, {{0, 1, 1, 0}, {0, 0, 1, 0}, 3}, {{2, 2, 2, 0}, {0, 1, 2, 0}, 3},
+    {{3, 3, 3, 3}, {0, 1, 2, 3}, 4}};
+constexpr int XF_NPAT = sizeof(XF_PAT) / sizeof(XF_PAT[0]);
+constexpr int XF_PAT_IDLE = 15;
+__host__ __device__ constexpr int xf_pat_frags(const XfPat& p) {
+  int m = 0;
+  for (int s = 0; s < p.n; ++s) m = std::max(m, std::max(p.a[s], p.b[s]) + 1);
+  return m;
+}
+__host__ __device__ constexpr int xf_pat_last_use(const XfPat& p, int q) {
+  int l = -1;
+  for (int s = 0; s < p.n; ++s)
+    if (p.a[s] == q || p.b[s] == q) l = s;
+  return l;
+}
+__host__ __device__ inline int xf_pat_blocks(int pat) { return XF_PAT[pat].n; }
+__host__ __device__ inline int xf_pat_a(int pat, int s) { return XF_PAT[pat].a[s]; }
+__host__ __device__ inline int xf_pat_b(int pat, int s) { return XF_PAT[pat].b[s]; }
+
+__global__ __launch_bounds__(XF_THREADS, 1) void kfac_factor_conv_x3f(FactorArgs args, ConvGeom cg) {
+  extern __shared__ __attribute__((aligned(16))) char cxf[];
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  const int task = xcd_task(blockIdx.x, gridDim.x);
+  int jx = 0;
+  while (jx + 1 < args.njobs && task >= args.task_end[jx]) ++jx;
+  const FactorJobDev& J = args.job[jx];
+  const OpDev& op = J.x;
+  const int split = task - J.task_begin;  // one unit: task = split
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t b0 = (int64_t)split * cg.B / J.splits, b1 = (int64_t)(split + 1) * cg.B / J.splits;
+  const int NV = cg.xf_nv, CL2 = cg.xf_cl * 2;  // variants, bytes per copy
+  const int partb = (cg.xf_ncp + 2) * CL2;      // one part: the copies, the ones copy, the zero copy
+  const int bufb = 3 * partb;
+  // once per task: zero both buffers, then the ones copies' hi parts (1 at p < L)
+  for (int e = tid; e < 2 * bufb / 16; e += XF_THREADS) reinterpret_cast<u32x4*>(cxf)[e] = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  if (cg.ones >= 0)
+    for (int e = tid; e < 2 * cg.L; e += XF_THREADS) {
+      const int bs = e / cg.L, p = e - bs * cg.L;
+      *reinterpret_cast<uint16_t*>(cxf + bs * bufb + cg.xf_ncp * CL2 + 2 * p) = 0x3f80;
+    }
+  // build slots (c, r, col): col even in padded coordinates; elements col .. col + 2 of
+  // padded row r of channel c, their pairs written to copy (c, kj) at ow = col - kj (kj
+  // even) or col + 1 - kj (kj odd), 0 <= ow < Wo (Wo even: a pair is wholly in or out).
+  // The slot's offsets are recomputed per use (held across the phases they cost the
+  // multiplying waves' registers)
+  constexpr int OUT = 0x7ffffff0;
+  const int wp2 = cg.xs_wp2, rowp = cg.xs_hp * wp2;
+  const int gt = tid % XF_GROUP, grp = wave / XF_GW;
+  const int nsp = (cg.xs_np + XF_GROUP - 1) / XF_GROUP;
+  struct Slot {
+    int c, r, col;
+    bool ok;
+  };
+  auto slot_of = [&](int i) __attribute__((always_inline)) {
+    const int e = gt + i * XF_GROUP;
+    Slot q;
+    q.ok = e < cg.xs_np;
+    const int ee = q.ok ? e : 0;
+    q.c = ee / rowp;
+    const int rem = ee - q.c * rowp;
+    q.r = rem / wp2;
+    q.col = 2 * (rem - q.r * wp2);
+    return q;
+  };
+  const int irec = op.C * op.H * op.W * 4;  // bytes of one image
+  float v0[XF_SP][3];
+  auto fetch = [&](int64_t b) __attribute__((always_inline)) {
+    const int seg = (int)((uint32_t)b / (uint32_t)cg.bseg);
+    const float* src = seg_base(J, args.segs, seg) + (b - (int64_t)seg * cg.bseg) * op.sB;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), 0, irec, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < XF_SP; ++i) {
+      if (i >= nsp) break;
+      const Slot q = slot_of(i);
+      const int h = q.r - op.ph;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const int w = q.col + d - op.pw;
+        const bool in = q.ok && h >= 0 && h < op.H && w >= 0 && w < op.W;
+        v0[i][d] = __uint_as_float(
+            __builtin_amdgcn_raw_buffer_load_b32(rs, in ? ((q.c * op.H + h) * op.W + w) * 4 : OUT, 0, 0));
+      }
+    }
+  };
+  // (running byte offsets: per-(kj, variant) constants hoisted out of the image loop
+  // spilled hundreds of SGPRs)
+  const int kstep = NV * CL2 - 2;  // bytes from (copy (c, kj), ow) to (copy (c, kj + 1), ow - 1)
+  const int vo0 = 2 * (cg.xf_smap & 3), vo1 = CL2 + 2 * ((cg.xf_smap >> 2) & 3);
+  auto build = [&](char* buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < XF_SP; ++i) {
+      if (i >= nsp) break;
+      const Slot q = slot_of(i);
+      if (!q.ok) continue;
+      uint32_t p0[3], p1[3];
+      split3(v0[i][0], v0[i][1], p0[0], p0[1], p0[2]);
+      split3(v0[i][1], v0[i][2], p1[0], p1[1], p1[2]);
+      char* d = buf + q.c * op.kw * NV * CL2 + (q.r * cg.Wo + q.col) * 2;
+      for (int kj = 0; kj < op.kw; ++kj, d += kstep) {
+        const int ow = q.col - kj + (kj & 1);
+        if (ow >= 0 && ow < cg.Wo) {
+          const bool odd = kj & 1;
+          char* dk = d + 2 * odd;
+#pragma unroll
+          for (int r = 0; r < 3; ++r) {
+            const uint32_t w = odd ? p1[r] : p0[r];
+            *reinterpret_cast<uint32_t*>(dk + vo0 + r * partb) = w;
+            if (NV > 1) *reinterpret_cast<uint32_t*>(dk + vo1 + r * partb) = w;
+          }
+        }
+      }
+    }
+  };
+  // this wave's fragment set F (<= 4 block rows of the factor: A of block (bi, bj) is
+  // fragment bi, B fragment bj -- one matrix) and its blocks as pairs of F indices, from
+  // a fixed menu of patterns (XF_PAT), so one k-step reads |F| fragments for up to 4
+  // blocks (LeNet-5's conv2: 14 fragment reads per k-step for 15 blocks instead of 30;
+  // at two 8-byte reads per fragment and part the LDS was the bound)
+  const int gw = wave % XF_GW, m = lane & 31, hh = lane >> 5;
+  auto row_off = [&](int f) __attribute__((always_inline)) {
+    if (f < op.cols) {
+      const int kk = op.kh * op.kw, c = f / kk, rr = f - c * kk, ki = rr / op.kw, kj = rr - ki * op.kw;
+      const int v = (cg.xf_vmap >> (2 * ki)) & 3, s = (cg.xf_smap >> (2 * v)) & 3;
+      return ((c * op.kw + kj) * NV + v) * CL2 + (ki * cg.Wo + s) * 2;
+    }
+    return (f == cg.ones ? cg.xf_ncp : cg.xf_ncp + 1) * CL2;
+  };
+  int wcode = 0;  // (constant-index reads of the argument: see mode 5)
+#pragma unroll
+  for (int t = 0; t < XF_GW; ++t) {
+    int e = cg.xf_wave[t];
+    asm volatile("" : "+s"(e));
+    wcode = gw == t ? e : wcode;
+  }
+  const int pat = wcode & 15;  // bits 4 + 3 q .. : F[q]
+  int offF[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) offF[q] = row_off(32 * ((wcode >> (4 + 3 * q)) & 7) + m) + 16 * hh;
+  floatx16 acc[XF_BPW];
+#pragma unroll
+  for (int i = 0; i < XF_BPW; ++i)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[i][v] = 0.f;
+  // the last k-step's positions past L (L even): fragments masked by dword where they
+  // are the A operand
+  const int nks = cg.xf_nks, last = nks - 1;
+  const int vc = min(max(cg.L - (16 * last + 8 * hh), 0), 8);
+  uint32_t amask[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) amask[d] = 2 * d + 1 < vc ? 0xffffffffu : 0u;
+  auto rd8 = [&](const char* p) __attribute__((always_inline)) {  // 8 bf16 from two 8-byte reads
+    const u32x2 lo = *reinterpret_cast<const u32x2*>(p), hi2 = *reinterpret_cast<const u32x2*>(p + 8);
+    return __builtin_bit_cast(bf16x8, u32x4{lo.x, lo.y, hi2.x, hi2.y});
+  };
+  auto mask_all = [&](X3Frag* F, int nf) __attribute__((always_inline)) {  // (in place)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q >= nf) break;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        u32x4 w = __builtin_bit_cast(u32x4, F[q].p[r]);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) w[d] &= amask[d];
+        F[q].p[r] = __builtin_bit_cast(bf16x8, w);
+      }
+    }
+  };
+  // one register set: after the block that uses a fragment last in this k-step, the
+  // fragment is reloaded for the next one, so each load has the following blocks'
+  // MFMAs to land (two whole sets of 4 fragments left no registers for the rest:
+  // spills).  The block orders of XF_PAT put a fragment's last use before the next
+  // k-step's first use wherever the pattern allows.  The last k-step's fragments are
+  // masked in place (a zero A or B element zeroes the product).
+  auto mma_pat = [&](const char* buf, auto PI) __attribute__((always_inline)) {
+    constexpr XfPat P = XF_PAT[decltype(PI)::value];
+    constexpr int NF = xf_pat_frags(P);
+    X3Frag F[NF];
+    auto load = [&](int t, int q) __attribute__((always_inline)) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) F[q].p[r] = rd8(buf + r * partb + offF[q] + 32 * t);
+    };
+    // (first reads in the loop's order -- by last use -- so the wait at the loop head
+    // holds for the entry as for the back edge; in fragment order it was lgkmcnt(0);
+    // the last k-step peeled: a mask at the loop head made every k-step wait for all
+    // of its reads)
+#pragma unroll
+    for (int s2 = 0; s2 < P.n; ++s2)
+#pragma unroll
+      for (int q = 0; q < NF; ++q)
+        if (xf_pat_last_use(P, q) == s2) load(0, q);
+    for (int t = 0; t < last; ++t) {
+#pragma unroll
+      for (int s2 = 0; s2 < P.n; ++s2) {
+        x3_six(acc[s2], F[P.a[s2]], F[P.b[s2]]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < NF; ++q)
+          if (xf_pat_last_use(P, q) == s2) load(t + 1, q);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    mask_all(F, NF);
+#pragma unroll
+    for (int s2 = 0; s2 < P.n; ++s2) x3_six(acc[s2], F[P.a[s2]], F[P.b[s2]]);
+  };
+  auto mma = [&](const char* buf) __attribute__((always_inline)) {
+    switch (pat) {
+      case 0: mma_pat(buf, std::integral_constant<int, 0>{}); break;
+      case 1: mma_pat(buf, std::integral_constant<int, 1>{}); break;
+      case 2: mma_pat(buf, std::integral_constant<int, 2>{}); break;
+      case 3: mma_pat(buf, std::integral_constant<int, 3>{}); break;
+      case 4: mma_pat(buf, std::integral_constant<int, 4>{}); break;
+      case 5: mma_pat(buf, std::integral_constant<int, 5>{}); break;
+      case 6: mma_pat(buf, std::integral_constant<int, 6>{}); break;
+      default: break;  // (XF_PAT_IDLE: no blocks)
+    }
+  };
+  // phases as mode 5: group i % 2 multiplies image i, the other builds image i + 1 and
+  // loads image i + 3; one straight-line loop per group
+  const int64_t nimg = b1 - b0;
+  auto phase_mma = [&](int64_t i) __attribute__((always_inline)) {
+    if (i < nimg) mma(cxf + (int)(i & 1) * bufb);
+    __syncthreads();
+  };
+  auto phase_build = [&](int64_t i) __attribute__((always_inline)) {
+    if (i + 1 < nimg) {
+      build(cxf + (int)((i + 1) & 1) * bufb);
+      if (i + 3 < nimg) fetch(b0 + i + 3);
+    }
+    __syncthreads();
+  };
+  if (grp == 0) {
+    if (nimg > 0) {
+      fetch(b0);
+      build(cxf);
+      if (nimg > 2) {
+        fetch(b0 + 2);
+#pragma unroll
+        for (int i = 0; i < XF_SP; ++i) asm volatile("" ::"v"(v0[i][0]), "v"(v0[i][1]), "v"(v0[i][2]));  // (landed)
+      }
+    }
+    __syncthreads();
+    for (int64_t i = 0; i < nimg; i += 2) {
+      phase_mma(i);
+      phase_build(i + 1);
+    }
+  } else {
+    if (nimg > 1) fetch(b0 + 1);
+    __syncthreads();
+    for (int64_t i = 0; i < nimg; i += 2) {
+      phase_build(i);
+      phase_mma(i + 1);
+    }
+  }
+  // group 1's partial sums added to group 0's (fixed order), then stored by group 0
+  float* red = reinterpret_cast<float*>(cxf);
+  const int nblk = pat < XF_NPAT ? xf_pat_blocks(pat) : 0;
+  if (grp == 1)
+#pragma unroll
+    for (int i = 0; i < XF_BPW; ++i)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) red[((gw * XF_BPW + i) * 16 + v) * 64 + lane] = acc[i][v];
+  __syncthreads();
+  if (grp == 1) return;
+#pragma unroll
+  for (int i = 0; i < XF_BPW; ++i) {
+    if (i >= nblk) break;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[i][v] += red[((gw * XF_BPW + i) * 16 + v) * 64 + lane];
+    const int bi = (wcode >> (4 + 3 * xf_pat_a(pat, i))) & 7, bj = (wcode >> (4 + 3 * xf_pat_b(pat, i))) & 7;
+    const int ti = bi >> 1, tj = bj >> 1;
+    float* o = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.sstride + split) * TILE * TILE +
+               (bi & 1) * 32 * TILE + (bj & 1) * 32;
+    put_partial(J, acc[i], [&](int v) { return &o[acc_row(v, lane) * TILE + (lane & 31)]; });
+  }
+}
+
 // Channel-major factors with n <= 8 (the G of a conv layer with few output
 // channels, e.g. LeNet-5's conv1: 6): F = sum over (image, position) of g g^T is
 // n(n+1)/2 FMAs per position against n loads -- an HBM stream, not MFMA work.  Each
@@ -2504,6 +2832,112 @@ static bool conv_x3s_geom(const kfac_operand& o, ConvGeom& g) {
   return true;
 }
 
+// Mode 6 (kfac_factor_conv_x3f): a stride-1 im2col operand with 32 < n <= 160 (<= 16
+// blocks: 4 per multiplying wave), even Wo (bf16 pairs), kernel <= 8 x 8, whose copies
+// fit twice in XF_LDS_MAX and take at most XF_SP build slots per thread.
+static bool conv_x3f_geom(const kfac_operand& o, ConvGeom& g) {
+  const int n = g.n;
+  if (n <= 32 || o.sh != 1 || o.sw != 1 || o.Ho <= 0 || o.Wo <= 0 || o.Wo % 2 != 0 || o.kw > XF_KW ||
+      o.kh > 8)
+    return false;
+  const int nb = (int)cdiv(n, 32), nq = nb * (nb + 1) / 2;
+  if (nb != 4 && nb != 5) return false;  // (the fragment-sharing assignments, XF_PAT)
+  const int hp = o.H + 2 * o.ph, wp2 = (o.W + 2 * o.pw + 1) / 2;
+  const int64_t np = (int64_t)o.C * hp * wp2;
+  if (np > (int64_t)XF_SP * XF_GROUP) return false;
+  // the shifts that align ki Wo + shift to 4 elements, one variant per distinct shift
+  int nv = 0, smap = 0, vmap = 0, shifts[4];
+  for (int ki = 0; ki < o.kh; ++ki) {
+    const int sft = (4 - (ki * o.Wo) % 4) % 4;
+    int v = 0;
+    while (v < nv && shifts[v] != sft) ++v;
+    if (v == nv) {
+      shifts[nv++] = sft;
+      smap |= sft << (2 * v);
+    }
+    vmap |= v << (2 * ki);
+  }
+  if (nv > 2) return false;  // (the build writes two variants at most)
+  const int ncp = o.C * o.kw * nv, ones = o.has_ones ? o.cols : -1;
+  // copy stride: the 8-byte reads of each 16-lane group (ds_read2_b64 / ds_read_b64
+  // bank rule: (a / 4) mod 32 in groups of 16 contiguous lanes) on distinct bank pairs
+  // as far as possible -- with the stride a multiple of 128 B every kj copy of a row
+  // fell on the same banks (5-way conflicts on LeNet-5's conv2: 3.8 vs 1.3 ms per pass)
+  auto row_off8 = [&](int f, int64_t cl) -> int64_t {  // fragment offset in 8-byte units
+    if (f < o.cols) {
+      const int kk = o.kh * o.kw, c = f / kk, rr = f - c * kk, ki = rr / o.kw, kj = rr - ki * o.kw;
+      const int v = (vmap >> (2 * ki)) & 3, sft = (smap >> (2 * v)) & 3;
+      return ((((int64_t)c * o.kw + kj) * nv + v) * cl + ki * o.Wo + sft) / 4;
+    }
+    return (f == ones ? ncp : ncp + 1) * cl / 4;
+  };
+  const int64_t cl0 = (hp * o.Wo + 20 + 3) / 4 * 4;
+  int best_w = 1 << 30;
+  int64_t cl = 0, bytes = 0;
+  for (int r = 0; r < 16; ++r) {
+    int64_t c4 = cl0 / 4;
+    while (c4 % 16 != r) ++c4;
+    const int64_t cand = 4 * c4, by = (int64_t)2 * 3 * (ncp + 2) * cand * 2;
+    if (by > XF_LDS_MAX) continue;
+    int worst = 0;  // distinct addresses on one bank pair (equal addresses broadcast)
+    for (int f0 = 0; f0 < 32 * nb; f0 += 16) {
+      int64_t seen[16][16];
+      int cnt[16] = {0};
+      for (int f = f0; f < f0 + 16; ++f) {
+        const int64_t a = row_off8(f, cand);
+        const int q = (int)(a % 16);
+        bool dup = false;
+        for (int t = 0; t < cnt[q]; ++t) dup |= seen[q][t] == a;
+        if (!dup) seen[q][cnt[q]++] = a;
+        worst = std::max(worst, cnt[q]);
+      }
+    }
+    if (worst < best_w || (worst == best_w && by < bytes)) {
+      best_w = worst;
+      cl = cand;
+      bytes = by;
+    }
+  }
+  if (best_w == 1 << 30) return false;
+  g.nb = nb;
+  g.nq = nq;
+  auto wave_code = [](int pat, std::initializer_list<int> f) {
+    int c = pat, q = 0;
+    for (int x : f) c |= x << (4 + 3 * q++);
+    return c;
+  };
+  if (nb == 5) {
+    g.xf_wave[0] = wave_code(0, {0, 1, 4});
+    g.xf_wave[1] = wave_code(1, {0, 1, 2, 3});
+    g.xf_wave[2] = wave_code(2, {0, 1, 2, 4});
+    g.xf_wave[3] = wave_code(3, {2, 3, 4});
+  } else {
+    g.xf_wave[0] = wave_code(4, {0, 1});
+    g.xf_wave[1] = wave_code(5, {0, 1, 2});
+    g.xf_wave[2] = wave_code(6, {0, 1, 2, 3});
+    g.xf_wave[3] = XF_PAT_IDLE;
+  }
+  g.xs_hp = hp;
+  g.xs_wp2 = wp2;
+  g.xs_np = (int)np;
+  g.xf_ncp = ncp;
+  g.xf_cl = (int)cl;
+  g.xf_nv = nv;
+  g.xf_smap = smap;
+  g.xf_vmap = vmap;
+  g.L = (int)o.L;
+  g.xf_nks = (int)cdiv(o.L, 16);
+  g.Wo = o.Wo;
+  g.sh = o.sh;
+  g.sw = o.sw;
+  g.ones = ones;
+  // (the epilogue's exchange: 4 waves x 4 blocks x 16 x 64 floats)
+  g.ldsb = (int)std::max<int64_t>(bytes, XF_GW * XF_BPW * 16 * 64 * 4);
+  g.mode = 6;
+  g.units = 1;
+  return true;
+}
+
 static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
   const kfac_operand& o = j.x;
   const int64_t nseg = j.nseg > 1 ? j.nseg : 1;
@@ -2515,7 +2949,9 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
   g.n = n;
   g.bseg = (int)(o.rows / o.L);
   g.B = (int)(nseg * g.bseg);
-  if (o.layout == KFAC_PATCH && knobs().conv_x3 && (conv_x3s_geom(o, g) || conv_x3_geom(o, g))) return true;
+  if (o.layout == KFAC_PATCH && knobs().conv_x3 &&
+      (conv_x3s_geom(o, g) || conv_x3f_geom(o, g) || conv_x3_geom(o, g)))
+    return true;
 constexpr int KFAC_CONV_NARROW32 = 3;  // n in 17..32: 3 = three 16x16 blocks, 1 = one 32x32 block (A/B)
   g.mode = n <= 16 ? 2 : (n <= 32 ? KFAC_CONV_NARROW32 : 0);
   g.KR = g.mode >= 2 ? 4 : 2;
@@ -2599,6 +3035,14 @@ static bool launch_conv_x3(const FactorArgs& args, const ConvGeom& g, int tasks,
 
 template <int LAYOUT>
 static void launch_conv(const FactorArgs& args, const ConvGeom& g, int tasks, hipStream_t stream) {
+  if (g.mode == 6) {
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&kfac_factor_conv_x3f),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 XF_LDS_MAX) == hipSuccess;
+    (void)attr;  // (a failed attribute surfaces as the launch error)
+    hipLaunchKernelGGL(kfac_factor_conv_x3f, dim3(tasks), dim3(XF_THREADS), (size_t)g.ldsb, stream, args, g);
+    return;
+  }
   if (g.mode == 5) {
     static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&kfac_factor_conv_x3s),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2930,7 +3374,7 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
       // larger cost there: conv1 G 15.7 / 12.4 / 13.2 us at k = 1 / 2 / 4)
       const bool small = jobs[i].x.layout == KFAC_CHANNEL && cg.n <= 8 && !conv_small_off();
       // (mode-0 instances are compiled for KFAC_CONV_OCC resident workgroups per CU;
-      // modes 4 and 5 run one 512-thread workgroup per CU)
+      // modes 4-6 run one 512-thread workgroup per CU)
       const int64_t cslots = cg.mode == 0 ? (int64_t)KFAC_CONV_OCC * 256 : cg.mode >= 4 ? 256 : slots;
       int k = (int)std::max<int64_t>(1, cdiv((int64_t)cg.units * cg.B, small ? cslots / 2 : cslots));
       if (knobs().conv_k > 0) k = knobs().conv_k;
@@ -3076,6 +3520,7 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
                      : !staged ? KFAC_PROF_FACTOR_TILES
                      : (jobs[0].x.layout == KFAC_CHANNEL && cg.n <= 8 && !conv_small_off())
                          ? KFAC_PROF_FACTOR_CHANNEL_SMALL
+                     : cg.mode == 6 ? KFAC_PROF_FACTOR_CONV_X3F
                      : cg.mode == 5 ? KFAC_PROF_FACTOR_CONV_X3S
                      : cg.mode == 4 ? KFAC_PROF_FACTOR_CONV_X3 : KFAC_PROF_FACTOR_CONV;
     double work = 0.0, bytes = 0.0;

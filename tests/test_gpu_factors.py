@@ -120,6 +120,9 @@ def test_conv_golden(hip_device):
         np.testing.assert_allclose(G.cpu().numpy(), g[f"G{li}"], **FT)
 
 
+X3F_SPECS = [(16, 6, 14, 14, 16, (5, 5), (1, 1), (0, 0), True), (64, 6, 14, 14, 16, (5, 5), (1, 1), (0, 0), True),
+             (3, 9, 5, 13, 5, (3, 4), (1, 1), (1, 2), True), (2, 10, 7, 8, 3, (3, 5), (1, 1), (1, 1), False),
+             (3, 4, 10, 11, 4, (6, 6), (1, 1), (1, 1), True)]
 X3S_SPECS = [(16, 1, 28, 28, 6, (5, 5), (1, 1), (2, 2), True), (256, 1, 28, 28, 6, (5, 5), (1, 1), (2, 2), True),
              (5, 2, 11, 13, 4, (3, 4), (2, 1), (1, 2), True),
              (3, 3, 12, 16, 5, (3, 3), (1, 1), (0, 1), False), (2, 2, 9, 9, 3, (4, 4), (1, 1), (1, 1), False)]
@@ -160,6 +163,14 @@ X3S_SPECS = [(16, 1, 28, 28, 6, (5, 5), (1, 1), (2, 2), True), (256, 1, 28, 28, 
     (3, 3, 12, 16, 5, (3, 3), (1, 1), (0, 1), False),
     (3, 3, 12, 17, 5, (3, 3), (1, 3), (0, 1), False),
     (2, 2, 9, 9, 3, (4, 4), (1, 1), (1, 1), False),
+    # kfac_factor_conv_x3f (stride-1 im2col factors with 97 <= n <= 160 from flattened
+    # column copies; LeNet-5's conv2 above): 4 block rows with two shifted variants (14
+    # output columns, 70 positions: a masked last k-step), 5 block rows without bias
+    # (two variants, 42 positions), 5 block rows with bias and a 6 x 6 kernel (one
+    # variant, 56 positions)
+    (3, 9, 5, 13, 5, (3, 4), (1, 1), (1, 2), True),
+    (2, 10, 7, 8, 3, (3, 5), (1, 1), (1, 1), False),
+    (3, 4, 10, 11, 4, (6, 6), (1, 1), (1, 1), True),
 ])
 def test_conv_shapes_vs_oracle(hip_device, spec):
     from bnn_kfac_amd import _native as N
@@ -179,6 +190,8 @@ def test_conv_shapes_vs_oracle(hip_device, spec):
     N.profile_enable(False)
     if spec in X3S_SPECS:  # the A factor on the column-copy kernel, one launch
         assert N.profile_read(N.PROF_FACTOR_CONV_X3S)[1] == 1
+    if spec in X3F_SPECS:  # on the flattened column-copy kernel
+        assert N.profile_read(N.PROF_FACTOR_CONV_X3F)[1] == 1
     A, G = kfac.state[conv]
     np.testing.assert_allclose(A.cpu().numpy(), O.conv_factor_A(x, k, p, s, bias, np.float64), **FT)
     np.testing.assert_allclose(G.cpu().numpy(), O.grad_factor(gr, np.float64), **FT)
