@@ -12,6 +12,10 @@
 //      F = beta*F + alpha*sum, write the tile and its mirror (LDS transpose),
 //      so F stays exactly symmetric.
 #include <algorithm>
+#include <cstddef>
+#include <array>
+#include <functional>
+#include <mutex>
 #include <initializer_list>
 #include <utility>
 #include <vector>
@@ -82,6 +86,33 @@ __device__ __forceinline__ void put_partial(const FactorJobDev& J, const floatx1
   for (int v = 0; v < 16; ++v) old[v] = *at(v);
 #pragma unroll
   for (int v = 0; v < 16; ++v) *at(v) = fmaf(J.sbeta, old[v], J.alpha * acc[v]);
+}
+
+// The same for the first nb of a wave's N blocks (`at(i, v)`: value v of block i), split
+// in two so the old values of every block are loaded before the first store (one round
+// trip to the slab instead of nb: the compiler keeps a block's loads behind the previous
+// block's stores) and can be in flight across the caller's partial-sum exchange.
+template <int N, class At>
+__device__ __forceinline__ void load_partials(const FactorJobDev& J, int nb, float (&old)[N][16], At at) {
+  if (!J.accum || J.sbeta == 0.f) return;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    if (i >= nb) break;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) old[i][v] = *at(i, v);
+  }
+}
+template <int N, class At>
+__device__ __forceinline__ void put_partials(const FactorJobDev& J, int nb, const floatx16 (&acc)[N],
+                                             const float (&old)[N][16], At at) {
+  const bool upd = J.accum && J.sbeta != 0.f;
+  const float a = J.accum ? J.alpha : 1.f;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    if (i >= nb) break;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) *at(i, v) = upd ? fmaf(J.sbeta, old[i][v], a * acc[i][v]) : a * acc[i][v];
+  }
 }
 
 // K is walked in BK-row stages; stage s of a job is rows [k, k + BK) of batch
@@ -1409,15 +1440,15 @@ struct ConvGeom {
   int xs_np;       // build slots per image (C xs_hp xs_wp2)
   int xs_wp2;      // build slots per padded row (ceil((W + 2 pw) / 2))
   // mode 6 (kfac_factor_conv_x3f: flattened column copies; xs_hp / xs_wp2 / xs_np too)
-  int xf_ncp;      // copies: C x kw x xf_nv (then the ones copy and the zero copy)
-  int xf_cl;       // bf16 per copy (Hp Wo + 20, multiple of 8)
   int xf_nv;       // shifted variants per copy (8-byte fragment reads)
-  int xf_smap;     // variant v's shift (elements) in bits 2v .. 2v+1
   int xf_vmap;     // kernel row ki's variant in bits 2ki .. 2ki+1
+  int xf_one, xf_zero, xf_dummy;  // part byte offsets of the ones / zero copies, the dummy row
   int xf_nks;      // 16-position k-steps per image (ceil(L / 16))
   int xf_wave[4];  // multiplying wave w: pattern (bits 0-3) and F[q] (bits 4 + 3q ..)
   int xs_lb[32];   // block row m's fragment byte offset in a part (copy, row, column)
   int8_t xs_f[32]; // block row m's factor row / column (data, bias, padding rows n..31)
+  // mode 6: copy (c, kj, v)'s part byte offset (shift included) in the u16 at 16 c + 2 kj + v
+  int xf_cb[128];
 };
 
 constexpr int KFAC_CONV_OCC = 4;  // resident workgroups per CU the mode-0 instances are compiled for
@@ -1969,6 +2000,17 @@ __global__ __launch_bounds__(CX3_THREADS, 1) void kfac_factor_conv_x3(FactorArgs
     }
   }
   __syncthreads();  // (every wave's last MFMA reads before the partial-sum exchange)
+  // block (bi, bj) = quadrant (bi & 1, bj & 1) of slab tile (bi / 2, bj / 2)
+  auto at = [&](int i, int v) __attribute__((always_inline)) {
+    int bi, bj;
+    tri_decode(block_of(i), bi, bj);
+    const int ti = bi >> 1, tj = bj >> 1;
+    float* o = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.sstride + split) * TILE * TILE +
+               (bi & 1) * 32 * TILE + (bj & 1) * 32;
+    return &o[acc_row(v, lane) * TILE + (lane & 31)];
+  };
+  float old[BPW][16];
+  if (kp == 0) load_partials(J, nmine, old, at);  // (in flight across the exchange)
   // kw > 1: the kw partial sums of a block meet in LDS (the im2col buffers are free
   // after the last barrier), summed in wave order by its first wave (deterministic)
   if (KW > 1) {
@@ -1982,17 +2024,7 @@ __global__ __launch_bounds__(CX3_THREADS, 1) void kfac_factor_conv_x3(FactorArgs
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[0][v] += red[(w * 16 + v) * 64 + lane];
   }
-  // block (bi, bj) = quadrant (bi & 1, bj & 1) of slab tile (bi / 2, bj / 2)
-#pragma unroll
-  for (int i = 0; i < BPW; ++i) {
-    if (i >= nmine) break;
-    int bi, bj;
-    tri_decode(block_of(i), bi, bj);
-    const int ti = bi >> 1, tj = bj >> 1;
-    float* o = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.sstride + split) * TILE * TILE +
-               (bi & 1) * 32 * TILE + (bj & 1) * 32;
-    put_partial(J, acc[i], [&](int v) { return &o[acc_row(v, lane) * TILE + (lane & 31)]; });
-  }
+  put_partials(J, nmine, acc, old, at);
 }
 
 // ------------------------------- one-block conv factors in bf16x3 (mode 5)
@@ -2278,17 +2310,21 @@ __global__ __launch_bounds__(XS_THREADS, 1) void kfac_factor_conv_x3s(FactorArgs
 // copies (kh x fewer entries than the im2col, 25 KB per LeNet-5 image in three bf16
 // parts instead of 102 KB) hold every MFMA fragment -- 8 consecutive positions of one
 // feature -- at element ki Wo + p.  8-byte reads need ki Wo + shift = 0 mod 4: each copy
-// is kept in NV <= 4 variants shifted by the residues the kernel rows need (LeNet-5
+// is kept in NV <= 2 variants shifted by the residues the kernel rows need (LeNet-5
 // conv2, Wo = 10: shifts 0 and 2).  Positions past L in the last 16-position k-step
-// read the next rows' data, so that k-step's A fragments are masked.  The bias row
-// reads a ones copy, padding rows a zero copy.
+// read the next rows' data, so that k-step's fragments are masked.  The bias row reads
+// a ones copy, padding rows a zero copy.
+// Copy placement (host, conv_x3f_geom): every copy (c, kj, v) has its own base, chosen so
+// the 8-byte fragment reads of each 16-lane group hit 16 distinct bank pairs (a search
+// over the bases' residues mod 128 B; a uniform copy stride left 2-way conflicts on 8 of
+// LeNet-5's 10 groups: the reads took twice their time, `profiles/r06z4/`).  The bases
+// sit in an LDS table (xf_cb, 16 entries per channel).
 // As in mode 5: one workgroup of 8 waves per CU, two copy buffers, two groups of 4
 // waves that swap roles every image (one multiplies image i, the other builds image
-// i + 1 and loads image i + 3); a multiplying wave takes blocks gw + 4 j of the lower
-// triangle (<= 4) over every k-step, the next (k-step, block) unit's fragments in
-// flight during the current one's MFMAs.  The build splits each image element once and
-// writes it (as bf16 pairs) to the kw NV copy slots that hold it.  At the end the two
-// groups' partial sums of a block meet in LDS (group 1's added to group 0's).
+// i + 1 and loads image i + 3).  The build works from per-slot records made once per
+// task (source offsets, destination offset, kernel columns in range): recomputing the
+// slot geometry per image (integer divisions) and a branch per copy made the build the
+// bound (3.9 us per image against 3.6 us of MFMAs; 425 VALU, 104 branches per wave).
 constexpr int XF_THREADS = 512;
 constexpr int XF_WAVES = XF_THREADS / 64;
 constexpr int XF_GROUP = XF_THREADS / 2;  // threads per role group
@@ -2296,7 +2332,13 @@ constexpr int XF_GW = XF_WAVES / 2;       // waves per role group
 constexpr int XF_SP = 3;                  // build slots per group thread and image (<= 768)
 constexpr int XF_BPW = 4;                 // blocks per multiplying wave (nq <= 16)
 constexpr int XF_KW = 8;                  // kernel width at most
-constexpr int XF_LDS_MAX = 134144;        // (a 29 KB inversion workgroup still fits beside it)
+constexpr int XF_CB = 256;                // copy-base table entries (C x 2 XF_KW: C <= 16)
+constexpr int XF_PART = 19456;            // bytes per part (copies, ones, zero, dummy)
+constexpr int XF_BUF = 3 * XF_PART;       // one copy buffer (hi, mid, lo parts)
+constexpr int XF_REC = 2 * XF_BUF;        // build-slot records: [slot i][group thread] u32x2
+constexpr int XF_TBL = XF_REC + XF_SP * XF_GROUP * 8;  // copy bases: u16 [c][kj][v] (v < 2)
+constexpr int XF_LDS = XF_TBL + XF_CB * 2;  // (a 29 KB inversion workgroup still fits beside it)
+static_assert(XF_LDS <= 134144 && XF_BUF >= XF_GW * XF_BPW * 16 * 64 * 4 / 2, "x3f LDS");
 
 // A multiplying wave's blocks as pairs (a, b) of indices into its fragment set F: block
 // (F[a], F[b]).  Assignments (conv_x3f_geom): 5 block rows (n = 129..160): waves take
@@ -2339,86 +2381,105 @@ __global__ __launch_bounds__(XF_THREADS, 1) void kfac_factor_conv_x3f(FactorArgs
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t b0 = (int64_t)split * cg.B / J.splits, b1 = (int64_t)(split + 1) * cg.B / J.splits;
-  const int NV = cg.xf_nv, CL2 = cg.xf_cl * 2;  // variants, bytes per copy
-  const int partb = (cg.xf_ncp + 2) * CL2;      // one part: the copies, the ones copy, the zero copy
-  const int bufb = 3 * partb;
-  // once per task: zero both buffers, then the ones copies' hi parts (1 at p < L)
-  for (int e = tid; e < 2 * bufb / 16; e += XF_THREADS) reinterpret_cast<u32x4*>(cxf)[e] = u32x4{0u, 0u, 0u, 0u};
+  const int gt = tid % XF_GROUP, grp = wave / XF_GW;
+  const int nsp = (cg.xs_np + XF_GROUP - 1) / XF_GROUP;
+  u32x2* rec = reinterpret_cast<u32x2*>(cxf + XF_REC);
+  uint16_t* tbl = reinterpret_cast<uint16_t*>(cxf + XF_TBL);
+  // once per task: zero both buffers; the copy-base table from the kernel argument
+  // (constant-index reads: a lane-indexed read of the argument copies it to scratch)
+  for (int e = tid; e < 2 * XF_BUF / 16; e += XF_THREADS) reinterpret_cast<u32x4*>(cxf)[e] = u32x4{0u, 0u, 0u, 0u};
+  if (tid < XF_CB / 2) {
+    // (read through the kernel-argument pointer: cg is the second argument, at its
+    // alignment after FactorArgs)
+    typedef const __attribute__((address_space(4))) char kchar;
+    typedef const __attribute__((address_space(4))) int kint;
+    kchar* ka = (kchar*)__builtin_amdgcn_kernarg_segment_ptr();
+    constexpr size_t cgo = (sizeof(FactorArgs) + alignof(ConvGeom) - 1) / alignof(ConvGeom) * alignof(ConvGeom);
+    reinterpret_cast<int*>(tbl)[tid] = ((kint*)(ka + cgo + offsetof(ConvGeom, xf_cb)))[tid];
+  }
+  // the build-slot records (c, r, col): col even in padded coordinates; elements col ..
+  // col + 2 of padded row r of channel c, their pairs written to copy (c, kj) at
+  // ow = col - kj (kj even) or col + 1 - kj (kj odd), 0 <= ow < Wo (Wo even: a pair is
+  // wholly in or out).  x: source dword + 8 (bits 0-15), elements in the image (bits
+  // 16-18); y: 2 (r Wo + col) (bits 0-15), c (16-23), kernel columns in range (24-31)
+  const int wp2 = cg.xs_wp2, rowp = cg.xs_hp * wp2;
+  if (tid < XF_GROUP)
+    for (int i = 0; i < nsp; ++i) {
+      const int e = tid + i * XF_GROUP;
+      uint32_t x = 0, y = 0;
+      if (e < cg.xs_np) {
+        const int c = e / rowp, rem = e - c * rowp, r = rem / wp2, col = 2 * (rem - r * wp2);
+        const int h = r - op.ph;
+        uint32_t dm = 0, km = 0;
+        for (int d = 0; d < 3; ++d) {
+          const int w = col + d - op.pw;
+          if (h >= 0 && h < op.H && w >= 0 && w < op.W) dm |= 1u << d;
+        }
+        for (int kj = 0; kj < op.kw; ++kj) {
+          const int ow = col - kj + (kj & 1);
+          if (ow >= 0 && ow < cg.Wo) km |= 1u << kj;
+        }
+        x = (uint32_t)(dm ? (c * op.H + h) * op.W + col - op.pw + 8 : 0) | dm << 16;
+        y = (uint32_t)(2 * (r * cg.Wo + col)) | (uint32_t)c << 16 | km << 24;
+      }
+      rec[i * XF_GROUP + tid] = u32x2{x, y};
+    }
   __syncthreads();
   if (cg.ones >= 0)
     for (int e = tid; e < 2 * cg.L; e += XF_THREADS) {
       const int bs = e / cg.L, p = e - bs * cg.L;
-      *reinterpret_cast<uint16_t*>(cxf + bs * bufb + cg.xf_ncp * CL2 + 2 * p) = 0x3f80;
+      *reinterpret_cast<uint16_t*>(cxf + bs * XF_BUF + cg.xf_one + 2 * p) = 0x3f80;
     }
-  // build slots (c, r, col): col even in padded coordinates; elements col .. col + 2 of
-  // padded row r of channel c, their pairs written to copy (c, kj) at ow = col - kj (kj
-  // even) or col + 1 - kj (kj odd), 0 <= ow < Wo (Wo even: a pair is wholly in or out).
-  // The slot's offsets are recomputed per use (held across the phases they cost the
-  // multiplying waves' registers)
   constexpr int OUT = 0x7ffffff0;
-  const int wp2 = cg.xs_wp2, rowp = cg.xs_hp * wp2;
-  const int gt = tid % XF_GROUP, grp = wave / XF_GW;
-  const int nsp = (cg.xs_np + XF_GROUP - 1) / XF_GROUP;
-  struct Slot {
-    int c, r, col;
-    bool ok;
-  };
-  auto slot_of = [&](int i) __attribute__((always_inline)) {
-    const int e = gt + i * XF_GROUP;
-    Slot q;
-    q.ok = e < cg.xs_np;
-    const int ee = q.ok ? e : 0;
-    q.c = ee / rowp;
-    const int rem = ee - q.c * rowp;
-    q.r = rem / wp2;
-    q.col = 2 * (rem - q.r * wp2);
-    return q;
-  };
   const int irec = op.C * op.H * op.W * 4;  // bytes of one image
   float v0[XF_SP][3];
-  auto fetch = [&](int64_t b) __attribute__((always_inline)) {
+  auto fetch = [&](int64_t b, const u32x2 (&rc)[XF_SP]) __attribute__((always_inline)) {
     const int seg = (int)((uint32_t)b / (uint32_t)cg.bseg);
     const float* src = seg_base(J, args.segs, seg) + (b - (int64_t)seg * cg.bseg) * op.sB;
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), 0, irec, 0x00020000);
 #pragma unroll
     for (int i = 0; i < XF_SP; ++i) {
       if (i >= nsp) break;
-      const Slot q = slot_of(i);
-      const int h = q.r - op.ph;
+      const int s0 = (int)(rc[i].x & 0xffffu) * 4 - 32;
 #pragma unroll
-      for (int d = 0; d < 3; ++d) {
-        const int w = q.col + d - op.pw;
-        const bool in = q.ok && h >= 0 && h < op.H && w >= 0 && w < op.W;
+      for (int d = 0; d < 3; ++d)
         v0[i][d] = __uint_as_float(
-            __builtin_amdgcn_raw_buffer_load_b32(rs, in ? ((q.c * op.H + h) * op.W + w) * 4 : OUT, 0, 0));
-      }
+            __builtin_amdgcn_raw_buffer_load_b32(rs, (rc[i].x >> (16 + d)) & 1u ? s0 + 4 * d : OUT, 0, 0));
     }
   };
-  // (running byte offsets: per-(kj, variant) constants hoisted out of the image loop
-  // spilled hundreds of SGPRs)
-  const int kstep = NV * CL2 - 2;  // bytes from (copy (c, kj), ow) to (copy (c, kj + 1), ow - 1)
-  const int vo0 = 2 * (cg.xf_smap & 3), vo1 = CL2 + 2 * ((cg.xf_smap >> 2) & 3);
-  auto build = [&](char* buf) __attribute__((always_inline)) {
+  auto records = [&](u32x2 (&rc)[XF_SP]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < XF_SP; ++i) rc[i] = i < nsp ? rec[i * XF_GROUP + gt] : u32x2{0u, 0u};
+  };
+  // out-of-range kernel columns write to a dummy row (one dword per lane) instead of a
+  // branch per copy
+  const int NV = cg.xf_nv, KW = op.kw;
+  const int dummy = cg.xf_dummy + 4 * lane;
+  auto build = [&](char* buf, const u32x2 (&rc)[XF_SP]) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < XF_SP; ++i) {
       if (i >= nsp) break;
-      const Slot q = slot_of(i);
-      if (!q.ok) continue;
       uint32_t p0[3], p1[3];
       split3(v0[i][0], v0[i][1], p0[0], p0[1], p0[2]);
       split3(v0[i][1], v0[i][2], p1[0], p1[1], p1[2]);
-      char* d = buf + q.c * op.kw * NV * CL2 + (q.r * cg.Wo + q.col) * 2;
-      for (int kj = 0; kj < op.kw; ++kj, d += kstep) {
-        const int ow = q.col - kj + (kj & 1);
-        if (ow >= 0 && ow < cg.Wo) {
-          const bool odd = kj & 1;
-          char* dk = d + 2 * odd;
+      const int q = (int)(rc[i].y & 0xffffu), c = (int)((rc[i].y >> 16) & 0xffu);
+      const uint32_t km = rc[i].y >> 24;
+      const u32x4* tb = reinterpret_cast<const u32x4*>(tbl + c * 2 * XF_KW);
+      const u32x4 t0 = tb[0], t1 = tb[1];  // this channel's copy bases, [kj][v]
 #pragma unroll
-          for (int r = 0; r < 3; ++r) {
-            const uint32_t w = odd ? p1[r] : p0[r];
-            *reinterpret_cast<uint32_t*>(dk + vo0 + r * partb) = w;
-            if (NV > 1) *reinterpret_cast<uint32_t*>(dk + vo1 + r * partb) = w;
-          }
+      for (int kj = 0; kj < XF_KW; ++kj) {
+        if (kj >= KW) break;
+        const uint32_t wv = kj < 4 ? t0[kj] : t1[kj - 4];
+        const bool in = (km >> kj) & 1u;
+        const int qk = q + 2 * ((kj & 1) - kj);
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          if (v >= NV) break;
+          const int base = (int)(v ? wv >> 16 : wv & 0xffffu);
+          char* d = buf + (in ? base + qk : dummy);
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+            *reinterpret_cast<uint32_t*>(d + r * XF_PART) = (kj & 1) ? p1[r] : p0[r];
         }
       }
     }
@@ -2432,10 +2493,10 @@ __global__ __launch_bounds__(XF_THREADS, 1) void kfac_factor_conv_x3f(FactorArgs
   auto row_off = [&](int f) __attribute__((always_inline)) {
     if (f < op.cols) {
       const int kk = op.kh * op.kw, c = f / kk, rr = f - c * kk, ki = rr / op.kw, kj = rr - ki * op.kw;
-      const int v = (cg.xf_vmap >> (2 * ki)) & 3, s = (cg.xf_smap >> (2 * v)) & 3;
-      return ((c * op.kw + kj) * NV + v) * CL2 + (ki * cg.Wo + s) * 2;
+      const int v = (cg.xf_vmap >> (2 * ki)) & 3;
+      return (int)tbl[c * 2 * XF_KW + 2 * kj + v] + 2 * ki * cg.Wo;
     }
-    return (f == cg.ones ? cg.xf_ncp : cg.xf_ncp + 1) * CL2;
+    return f == cg.ones ? cg.xf_one : cg.xf_zero;
   };
   int wcode = 0;  // (constant-index reads of the argument: see mode 5)
 #pragma unroll
@@ -2453,8 +2514,7 @@ __global__ __launch_bounds__(XF_THREADS, 1) void kfac_factor_conv_x3f(FactorArgs
   for (int i = 0; i < XF_BPW; ++i)
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[i][v] = 0.f;
-  // the last k-step's positions past L (L even): fragments masked by dword where they
-  // are the A operand
+  // the last k-step's positions past L (L even): fragments masked by dword
   const int nks = cg.xf_nks, last = nks - 1;
   const int vc = min(max(cg.L - (16 * last + 8 * hh), 0), 8);
   uint32_t amask[4];
@@ -2489,7 +2549,7 @@ __global__ __launch_bounds__(XF_THREADS, 1) void kfac_factor_conv_x3f(FactorArgs
     X3Frag F[NF];
     auto load = [&](int t, int q) __attribute__((always_inline)) {
 #pragma unroll
-      for (int r = 0; r < 3; ++r) F[q].p[r] = rd8(buf + r * partb + offF[q] + 32 * t);
+      for (int r = 0; r < 3; ++r) F[q].p[r] = rd8(buf + r * XF_PART + offF[q] + 32 * t);
     };
     // (first reads in the loop's order -- by last use -- so the wait at the loop head
     // holds for the entry as for the back edge; in fragment order it was lgkmcnt(0);
@@ -2531,22 +2591,26 @@ __global__ __launch_bounds__(XF_THREADS, 1) void kfac_factor_conv_x3f(FactorArgs
   // loads image i + 3; one straight-line loop per group
   const int64_t nimg = b1 - b0;
   auto phase_mma = [&](int64_t i) __attribute__((always_inline)) {
-    if (i < nimg) mma(cxf + (int)(i & 1) * bufb);
+    if (i < nimg) mma(cxf + (int)(i & 1) * XF_BUF);
     __syncthreads();
   };
   auto phase_build = [&](int64_t i) __attribute__((always_inline)) {
     if (i + 1 < nimg) {
-      build(cxf + (int)((i + 1) & 1) * bufb);
-      if (i + 3 < nimg) fetch(b0 + i + 3);
+      u32x2 rc[XF_SP];
+      records(rc);
+      build(cxf + (int)((i + 1) & 1) * XF_BUF, rc);
+      if (i + 3 < nimg) fetch(b0 + i + 3, rc);
     }
     __syncthreads();
   };
   if (grp == 0) {
     if (nimg > 0) {
-      fetch(b0);
-      build(cxf);
+      u32x2 rc[XF_SP];
+      records(rc);
+      fetch(b0, rc);
+      build(cxf, rc);
       if (nimg > 2) {
-        fetch(b0 + 2);
+        fetch(b0 + 2, rc);
 #pragma unroll
         for (int i = 0; i < XF_SP; ++i) asm volatile("" ::"v"(v0[i][0]), "v"(v0[i][1]), "v"(v0[i][2]));  // (landed)
       }
@@ -2557,7 +2621,11 @@ __global__ __launch_bounds__(XF_THREADS, 1) void kfac_factor_conv_x3f(FactorArgs
       phase_build(i + 1);
     }
   } else {
-    if (nimg > 1) fetch(b0 + 1);
+    if (nimg > 1) {
+      u32x2 rc[XF_SP];
+      records(rc);
+      fetch(b0 + 1, rc);
+    }
     __syncthreads();
     for (int64_t i = 0; i < nimg; i += 2) {
       phase_build(i);
@@ -2565,13 +2633,25 @@ __global__ __launch_bounds__(XF_THREADS, 1) void kfac_factor_conv_x3f(FactorArgs
     }
   }
   // group 1's partial sums added to group 0's (fixed order), then stored by group 0
+  // (group 0's accumulator reads in flight across the exchange)
   float* red = reinterpret_cast<float*>(cxf);
   const int nblk = pat < XF_NPAT ? xf_pat_blocks(pat) : 0;
-  if (grp == 1)
+  auto at = [&](int i, int v) __attribute__((always_inline)) {
+    const int bi = (wcode >> (4 + 3 * xf_pat_a(pat, i))) & 7, bj = (wcode >> (4 + 3 * xf_pat_b(pat, i))) & 7;
+    const int ti = bi >> 1, tj = bj >> 1;
+    float* o = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.sstride + split) * TILE * TILE +
+               (bi & 1) * 32 * TILE + (bj & 1) * 32;
+    return &o[acc_row(v, lane) * TILE + (lane & 31)];
+  };
+  float old[XF_BPW][16];
+  if (grp == 1) {
 #pragma unroll
     for (int i = 0; i < XF_BPW; ++i)
 #pragma unroll
       for (int v = 0; v < 16; ++v) red[((gw * XF_BPW + i) * 16 + v) * 64 + lane] = acc[i][v];
+  } else {
+    load_partials(J, nblk, old, at);
+  }
   __syncthreads();
   if (grp == 1) return;
 #pragma unroll
@@ -2579,12 +2659,8 @@ __global__ __launch_bounds__(XF_THREADS, 1) void kfac_factor_conv_x3f(FactorArgs
     if (i >= nblk) break;
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[i][v] += red[((gw * XF_BPW + i) * 16 + v) * 64 + lane];
-    const int bi = (wcode >> (4 + 3 * xf_pat_a(pat, i))) & 7, bj = (wcode >> (4 + 3 * xf_pat_b(pat, i))) & 7;
-    const int ti = bi >> 1, tj = bj >> 1;
-    float* o = J.slab + ((size_t)(ti * (ti + 1) / 2 + tj) * J.sstride + split) * TILE * TILE +
-               (bi & 1) * 32 * TILE + (bj & 1) * 32;
-    put_partial(J, acc[i], [&](int v) { return &o[acc_row(v, lane) * TILE + (lane & 31)]; });
   }
+  put_partials(J, nblk, acc, old, at);
 }
 
 // Channel-major factors with n <= 8 (the G of a conv layer with few output
@@ -2833,72 +2909,139 @@ static bool conv_x3s_geom(const kfac_operand& o, ConvGeom& g) {
 }
 
 // Mode 6 (kfac_factor_conv_x3f): a stride-1 im2col operand with 32 < n <= 160 (<= 16
-// blocks: 4 per multiplying wave), even Wo (bf16 pairs), kernel <= 8 x 8, whose copies
-// fit twice in XF_LDS_MAX and take at most XF_SP build slots per thread.
+// blocks: 4 per multiplying wave), even Wo (bf16 pairs), kernel <= 8 x 8, C <= 16, whose
+// copies fit in XF_PART and take at most XF_SP build slots per thread.
+// Copy bases: the fragment row of feature (c, ki, kj) starts at 8-byte unit
+// base(c, kj, v(ki)) + (ki Wo + shift) / 4; a 16-lane group of ds_read_b64 / ds_read2_b64
+// is conflict-free when its 16 distinct units are distinct mod 16 (equal addresses
+// broadcast: the zero rows).  A depth-first search over the copies' residues mod 16
+// (in order of first use, <= 2^20 nodes) finds such bases (LeNet-5's conv2: 15 k nodes),
+// then the copies are laid out in a chain that keeps the gaps between them small.
+static bool xf_place(const kfac_operand& o, int nb, int nv, int vmap, const int* sft, int zo, int* res) {
+  const int ncp = o.C * o.kw * nv, nc = ncp + 1;  // + the ones / zero region
+  const int ones = o.has_ones ? o.cols : -1, ng = 2 * nb;
+  auto feat = [&](int f, int& cp, int& off) {
+    if (f < o.cols) {
+      const int kk = o.kh * o.kw, c = f / kk, rr = f - c * kk, ki = rr / o.kw, kj = rr - ki * o.kw;
+      const int v = (vmap >> (2 * ki)) & 3;
+      cp = (c * o.kw + kj) * nv + v;
+      off = (ki * o.Wo + sft[v]) / 4;
+    } else {
+      cp = ncp;
+      off = f == ones ? 0 : zo;
+    }
+  };
+  // uses[cp]: (group, offset) pairs, distinct
+  std::vector<std::vector<std::pair<int, int>>> uses(nc);
+  std::vector<int> first(nc, 1 << 30);
+  for (int g = 0; g < ng; ++g)
+    for (int f = 16 * g; f < 16 * g + 16; ++f) {
+      int cp, off;
+      feat(f, cp, off);
+      bool dup = false;
+      for (auto& u : uses[cp]) dup |= u.first == g && u.second == off;
+      if (!dup) uses[cp].push_back({g, off});
+      first[cp] = std::min(first[cp], g);
+    }
+  std::vector<int> order(nc);
+  for (int i = 0; i < nc; ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return first[x] < first[y]; });
+  std::vector<uint16_t> used(ng, 0);
+  int64_t nodes = 0;
+  std::function<bool(int)> dfs = [&](int k) -> bool {
+    if (k == nc) return true;
+    if (++nodes > (1 << 20)) return false;
+    const int i = order[k];
+    for (int r = 0; r < 16; ++r) {
+      bool ok = true;
+      for (auto& u : uses[i]) ok &= !((used[u.first] >> ((r + u.second) & 15)) & 1);
+      if (!ok) continue;
+      for (auto& u : uses[i]) used[u.first] |= (uint16_t)(1u << ((r + u.second) & 15));
+      res[i] = r;
+      if (dfs(k + 1)) return true;
+      for (auto& u : uses[i]) used[u.first] &= (uint16_t)~(1u << ((r + u.second) & 15));
+    }
+    return false;
+  };
+  return dfs(0);
+}
+
+static bool conv_x3f_geom_new(const kfac_operand& o, ConvGeom& g);
+// (the plan is made per call: the residue search and layout are memoized per shape --
+// uncached they cost 7 ms per LeNet-5 pass)
 static bool conv_x3f_geom(const kfac_operand& o, ConvGeom& g) {
+  typedef std::array<int64_t, 12> Key;
+  static std::mutex mu;
+  static std::vector<std::pair<Key, std::pair<bool, ConvGeom>>> memo;
+  const Key k{o.C, o.H, o.W, o.kh, o.kw, o.ph, o.pw, o.sh, o.sw, o.Ho * 65536 + o.Wo, o.cols * 2 + (o.has_ones ? 1 : 0),
+              (int64_t)g.n};
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto& e : memo)
+      if (e.first == k) {
+        if (!e.second.first) return false;
+        ConvGeom r = e.second.second;
+        // (the fields set before this search: kept from the caller)
+        r.B = g.B;
+        r.bseg = g.bseg;
+        g = r;
+        return true;
+      }
+  }
+  ConvGeom r = g;
+  const bool ok = conv_x3f_geom_new(o, r);
+  std::lock_guard<std::mutex> lk(mu);
+  if (memo.size() < 64) memo.push_back({k, {ok, r}});
+  if (ok) g = r;
+  return ok;
+}
+
+static bool conv_x3f_geom_new(const kfac_operand& o, ConvGeom& g) {
   const int n = g.n;
   if (n <= 32 || o.sh != 1 || o.sw != 1 || o.Ho <= 0 || o.Wo <= 0 || o.Wo % 2 != 0 || o.kw > XF_KW ||
-      o.kh > 8)
+      o.kh > 8 || o.C > XF_CB / (2 * XF_KW) || (int64_t)o.C * o.H * o.W + 16 > 0xffff)
     return false;
   const int nb = (int)cdiv(n, 32), nq = nb * (nb + 1) / 2;
   if (nb != 4 && nb != 5) return false;  // (the fragment-sharing assignments, XF_PAT)
   const int hp = o.H + 2 * o.ph, wp2 = (o.W + 2 * o.pw + 1) / 2;
   const int64_t np = (int64_t)o.C * hp * wp2;
-  if (np > (int64_t)XF_SP * XF_GROUP) return false;
+  if (np > (int64_t)XF_SP * XF_GROUP || 2 * (hp * o.Wo + 2 * wp2) > 0xffff) return false;
   // the shifts that align ki Wo + shift to 4 elements, one variant per distinct shift
-  int nv = 0, smap = 0, vmap = 0, shifts[4];
+  int nv = 0, vmap = 0, shifts[4];
   for (int ki = 0; ki < o.kh; ++ki) {
     const int sft = (4 - (ki * o.Wo) % 4) % 4;
     int v = 0;
     while (v < nv && shifts[v] != sft) ++v;
-    if (v == nv) {
-      shifts[nv++] = sft;
-      smap |= sft << (2 * v);
-    }
+    if (v == nv) shifts[nv++] = sft;
     vmap |= v << (2 * ki);
   }
   if (nv > 2) return false;  // (the build writes two variants at most)
-  const int ncp = o.C * o.kw * nv, ones = o.has_ones ? o.cols : -1;
-  // copy stride: the 8-byte reads of each 16-lane group (ds_read2_b64 / ds_read_b64
-  // bank rule: (a / 4) mod 32 in groups of 16 contiguous lanes) on distinct bank pairs
-  // as far as possible -- with the stride a multiple of 128 B every kj copy of a row
-  // fell on the same banks (5-way conflicts on LeNet-5's conv2: 3.8 vs 1.3 ms per pass)
-  auto row_off8 = [&](int f, int64_t cl) -> int64_t {  // fragment offset in 8-byte units
-    if (f < o.cols) {
-      const int kk = o.kh * o.kw, c = f / kk, rr = f - c * kk, ki = rr / o.kw, kj = rr - ki * o.kw;
-      const int v = (vmap >> (2 * ki)) & 3, sft = (smap >> (2 * v)) & 3;
-      return ((((int64_t)c * o.kw + kj) * nv + v) * cl + ki * o.Wo + sft) / 4;
+  const int ncp = o.C * o.kw * nv;
+  const int nks = (int)cdiv(o.L, 16);
+  const int cu = (hp * o.Wo + 3 + 3) / 4;  // 8-byte units per copy (elements shift .. shift + Hp Wo)
+  const int zo = 4 * nks + 2;               // the zero copy after the ones copy (units)
+  std::vector<int> res(ncp + 1);
+  if (!xf_place(o, nb, nv, vmap, shifts, zo, res.data())) return false;
+  // chain layout: the next copy is the one whose residue is reached with the least gap
+  std::vector<std::vector<int>> pool(16);
+  for (int i = ncp - 1; i >= 0; --i) pool[res[i]].push_back(i);
+  std::vector<int> base(ncp + 1);
+  int p = 0;
+  for (int left = ncp; left > 0; --left)
+    for (int gap = 0; gap < 16; ++gap) {
+      auto& q = pool[(p + gap) & 15];
+      if (q.empty()) continue;
+      base[q.back()] = p + gap;
+      q.pop_back();
+      p += gap + cu;
+      break;
     }
-    return (f == ones ? ncp : ncp + 1) * cl / 4;
-  };
-  const int64_t cl0 = (hp * o.Wo + 20 + 3) / 4 * 4;
-  int best_w = 1 << 30;
-  int64_t cl = 0, bytes = 0;
-  for (int r = 0; r < 16; ++r) {
-    int64_t c4 = cl0 / 4;
-    while (c4 % 16 != r) ++c4;
-    const int64_t cand = 4 * c4, by = (int64_t)2 * 3 * (ncp + 2) * cand * 2;
-    if (by > XF_LDS_MAX) continue;
-    int worst = 0;  // distinct addresses on one bank pair (equal addresses broadcast)
-    for (int f0 = 0; f0 < 32 * nb; f0 += 16) {
-      int64_t seen[16][16];
-      int cnt[16] = {0};
-      for (int f = f0; f < f0 + 16; ++f) {
-        const int64_t a = row_off8(f, cand);
-        const int q = (int)(a % 16);
-        bool dup = false;
-        for (int t = 0; t < cnt[q]; ++t) dup |= seen[q][t] == a;
-        if (!dup) seen[q][cnt[q]++] = a;
-        worst = std::max(worst, cnt[q]);
-      }
-    }
-    if (worst < best_w || (worst == best_w && by < bytes)) {
-      best_w = worst;
-      cl = cand;
-      bytes = by;
-    }
-  }
-  if (best_w == 1 << 30) return false;
+  while ((p & 15) != res[ncp]) ++p;
+  base[ncp] = p;
+  // ones copy, zero copy (16 nks + 8 bf16 of reads each), the dummy row (64 dwords, and
+  // the last k-step's over-reads past any copy land before the part's end)
+  const int dummy = 8 * (p + zo + 4 * nks + 4);
+  if (dummy + 256 + 64 > XF_PART) return false;
   g.nb = nb;
   g.nq = nq;
   auto wave_code = [](int pat, std::initializer_list<int> f) {
@@ -2920,19 +3063,24 @@ static bool conv_x3f_geom(const kfac_operand& o, ConvGeom& g) {
   g.xs_hp = hp;
   g.xs_wp2 = wp2;
   g.xs_np = (int)np;
-  g.xf_ncp = ncp;
-  g.xf_cl = (int)cl;
   g.xf_nv = nv;
-  g.xf_smap = smap;
   g.xf_vmap = vmap;
+  for (int c = 0; c < o.C; ++c)
+    for (int kj = 0; kj < o.kw; ++kj)
+      for (int v = 0; v < nv; ++v) {
+        const int e = 16 * c + 2 * kj + v, b = 8 * base[(c * o.kw + kj) * nv + v] + 2 * shifts[v];
+        g.xf_cb[e / 2] |= b << (16 * (e & 1));
+      }
+  g.xf_one = 8 * base[ncp];
+  g.xf_zero = 8 * (base[ncp] + zo);
+  g.xf_dummy = dummy;
   g.L = (int)o.L;
-  g.xf_nks = (int)cdiv(o.L, 16);
+  g.xf_nks = nks;
   g.Wo = o.Wo;
   g.sh = o.sh;
   g.sw = o.sw;
-  g.ones = ones;
-  // (the epilogue's exchange: 4 waves x 4 blocks x 16 x 64 floats)
-  g.ldsb = (int)std::max<int64_t>(bytes, XF_GW * XF_BPW * 16 * 64 * 4);
+  g.ones = o.has_ones ? o.cols : -1;
+  g.ldsb = XF_LDS;
   g.mode = 6;
   g.units = 1;
   return true;
@@ -3038,7 +3186,7 @@ static void launch_conv(const FactorArgs& args, const ConvGeom& g, int tasks, hi
   if (g.mode == 6) {
     static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&kfac_factor_conv_x3f),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 XF_LDS_MAX) == hipSuccess;
+                                                 XF_LDS) == hipSuccess;
     (void)attr;  // (a failed attribute surfaces as the launch error)
     hipLaunchKernelGGL(kfac_factor_conv_x3f, dim3(tasks), dim3(XF_THREADS), (size_t)g.ldsb, stream, args, g);
     return;
