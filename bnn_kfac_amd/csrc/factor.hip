@@ -3524,7 +3524,10 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
       // (mode-0 instances are compiled for KFAC_CONV_OCC resident workgroups per CU;
       // modes 4-6 run one 512-thread workgroup per CU)
       const int64_t cslots = cg.mode == 0 ? (int64_t)KFAC_CONV_OCC * 256 : cg.mode >= 4 ? 256 : slots;
-      int k = (int)std::max<int64_t>(1, cdiv((int64_t)cg.units * cg.B, small ? cslots / 2 : cslots));
+      // (a multi-batch launch -- thousands of images -- amortizes that reduction: the n <= 8
+      // kernel then takes 4 workgroups per CU, twice the loads in flight of 2)
+      const bool halve = small && cg.B <= 8 * cslots;
+      int k = (int)std::max<int64_t>(1, cdiv((int64_t)cg.units * cg.B, halve ? cslots / 2 : cslots));
       if (knobs().conv_k > 0) k = knobs().conv_k;
       k = std::min(k, cg.B);
       p.splits = (int)cdiv(cg.B, k);
