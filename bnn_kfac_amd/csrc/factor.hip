@@ -2690,30 +2690,38 @@ __global__ __launch_bounds__(NTHREADS) void kfac_factor_channel_small(FactorArgs
   float acc[NT];
 #pragma unroll
   for (int e = 0; e < NT; ++e) acc[e] = 0.f;
-  // two (image, run) pairs per trip, their 2 x n float4 loads issued together
+  // PP (image, run) pairs per trip, their PP x n float4 loads issued together
+  constexpr int PP = 2;
   auto src_of = [&](uint32_t q) {
     const uint32_t img = q / L4, r4 = q - img * L4;
     // image b0 + img of the job: batch seg of the queued batches, image bi in it
     const uint32_t ab = (uint32_t)b0 + img, seg = ab / (uint32_t)cg.bseg;
     return seg_base(J, args.segs, (int)seg) + (int64_t)(ab - seg * cg.bseg) * op.sB + 4 * r4;
   };
-  for (uint32_t q = tid; q < per; q += 2 * NTHREADS) {
-    const bool two = q + NTHREADS < per;
-    const float* s0 = src_of(q);
-    const float* s1 = two ? src_of(q + NTHREADS) : s0;
-    floatx4 x[2][NMAX];
+  for (uint32_t q = tid; q < per; q += PP * NTHREADS) {
+    const float* sp[PP];
+    bool ok[PP];
 #pragma unroll
-    for (int c = 0; c < NMAX; ++c) {
-      const bool in = c < n;  // (channels past n: zero rows of the triangle)
-      x[0][c] = in ? *reinterpret_cast<const floatx4*>(s0 + c * op.L) : floatx4{0.f, 0.f, 0.f, 0.f};
-      x[1][c] = in ? *reinterpret_cast<const floatx4*>(s1 + c * op.L) : floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int h = 0; h < PP; ++h) {
+      ok[h] = h == 0 || q + h * NTHREADS < per;
+      sp[h] = ok[h] ? src_of(q + h * NTHREADS) : sp[0];
     }
-    if (!two) {
+    floatx4 x[PP][NMAX];
 #pragma unroll
-      for (int c = 0; c < NMAX; ++c) x[1][c] = floatx4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int c = 0; c < NMAX; ++c)
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+      for (int h = 0; h < PP; ++h) {
+        const bool in = c < n;  // (channels past n: zero rows of the triangle)
+        x[h][c] = in ? *reinterpret_cast<const floatx4*>(sp[h] + c * op.L) : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+    for (int h = 1; h < PP; ++h)
+      if (!ok[h]) {
+#pragma unroll
+        for (int c = 0; c < NMAX; ++c) x[h][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+    for (int h = 0; h < PP; ++h)
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -2749,6 +2757,10 @@ __global__ __launch_bounds__(NTHREADS) void kfac_factor_channel_small(FactorArgs
 
 // KFAC_CONV_SMALL=0: channel factors with n <= 8 on the MFMA kernel (A/B checks)
 static bool conv_small_off() { return !knobs().conv_small; }
+// the register-triangle kernel takes channel factors with n <= 8 (an n = 16 instance --
+// 136 sums per thread, 256 VGPRs -- ran LeNet-5's conv2 G at 0.63 ms per pass against
+// 0.17 on the MFMA kernel, `profiles/r06z10/`)
+static bool channel_small(const ConvGeom& g) { return !conv_small_off() && g.n <= 8; }
 
 // Geometry of a conv job on the LDS-staged kernel; false: the job takes the
 // register-staged path (images too large, channel blocks not float4-shaped, or an
@@ -3207,7 +3219,7 @@ static void launch_conv(const FactorArgs& args, const ConvGeom& g, int tasks, hi
     (void)ok;  // (a failed attribute surfaces as the launch error below)
     return;
   }
-  if (LAYOUT == KFAC_CHANNEL && g.n <= 8 && !conv_small_off()) {
+  if (LAYOUT == KFAC_CHANNEL && channel_small(g)) {
     // the exact channel count (LeNet-5 conv1: 6) sizes the register triangle and its
     // reduction; other counts take the next instance up (their extra rows are zero)
     if (g.n == 6)
@@ -3520,7 +3532,7 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
       // `git show e37cdaa^:tools/microbench/conv_ab.hip`, KFAC_CONV_K overrides k)
       // (the n <= 8 channel kernel: half the slots -- its per-task reduction is the
       // larger cost there: conv1 G 15.7 / 12.4 / 13.2 us at k = 1 / 2 / 4)
-      const bool small = jobs[i].x.layout == KFAC_CHANNEL && cg.n <= 8 && !conv_small_off();
+      const bool small = jobs[i].x.layout == KFAC_CHANNEL && channel_small(cg);
       // (mode-0 instances are compiled for KFAC_CONV_OCC resident workgroups per CU;
       // modes 4-6 run one 512-thread workgroup per CU)
       const int64_t cslots = cg.mode == 0 ? (int64_t)KFAC_CONV_OCC * 256 : cg.mode >= 4 ? 256 : slots;
@@ -3669,7 +3681,7 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
     // launch's algorithmic flops: sum over jobs of K rows x n (n + 1)
     const int slot = s3 ? KFAC_PROF_FACTOR_SYRK3 : x3 ? KFAC_PROF_FACTOR_X3
                      : !staged ? KFAC_PROF_FACTOR_TILES
-                     : (jobs[0].x.layout == KFAC_CHANNEL && cg.n <= 8 && !conv_small_off())
+                     : (jobs[0].x.layout == KFAC_CHANNEL && channel_small(cg))
                          ? KFAC_PROF_FACTOR_CHANNEL_SMALL
                      : cg.mode == 6 ? KFAC_PROF_FACTOR_CONV_X3F
                      : cg.mode == 5 ? KFAC_PROF_FACTOR_CONV_X3S

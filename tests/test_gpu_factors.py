@@ -197,6 +197,31 @@ def test_conv_shapes_vs_oracle(hip_device, spec):
     np.testing.assert_allclose(G.cpu().numpy(), O.grad_factor(gr, np.float64), **FT)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("cout", [6, 7])
+def test_channel_small_large_launch(hip_device, cout):
+    """G of a conv layer over 9,000 images in one launch (the n <= 8 register-triangle
+    kernel at 4 workgroups per CU past 8,192 images; 7: the n = 8 instance with a zero
+    row)."""
+    from bnn_kfac_amd import _native as N
+    from bnn_kfac_amd.curvatures import KFAC
+    B, Ho, Wo = 9000, 10, 10
+    rng = np.random.default_rng(cout)
+    conv = nn.Conv2d(3, cout, 3, bias=True).to(hip_device)
+    x = rng.random((B, 3, Ho + 2, Wo + 2), dtype=np.float32)
+    gr = rng.standard_normal((B, cout, Ho, Wo), dtype=np.float32)
+    kfac = KFAC(conv)
+    kfac.record[conv] = [_t(x, hip_device), _t(gr, hip_device)]
+    N.profile_reset()
+    N.profile_enable(True)
+    kfac.update(batch_size=B)
+    torch.cuda.synchronize()
+    N.profile_enable(False)
+    assert N.profile_read(N.PROF_FACTOR_CHANNEL_SMALL)[1] == 1
+    _, G = kfac.state[conv]
+    np.testing.assert_allclose(G.cpu().numpy(), O.grad_factor(gr, np.float64), **FT)
+
+
 def test_hooks_end_to_end_basenet750(hip_device):
     """Full forward/backward through the hooks reproduces the reference's factors (G5)."""
     from bnn_kfac_amd.curvatures import KFAC
