@@ -904,6 +904,16 @@ __device__ __forceinline__ void x3_six(floatx16& acc, const X3Frag& A, const X3F
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.p[0], B.p[0], acc, 0, 0, 0);
 }
 
+// The same for a diagonal block (A = B): the cross products come in transposed pairs
+// (lo hi^T and hi lo^T, mid hi^T and hi mid^T), so four MFMAs -- hh + mm into acc,
+// (lo + mid) hi^T into acc2 -- and the caller adds acc2 + acc2^T once at the end.
+__device__ __forceinline__ void x3_four(floatx16& acc, floatx16& acc2, const X3Frag& A) {
+  acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.p[2], A.p[0], acc2, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.p[1], A.p[1], acc, 0, 0, 0);
+  acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.p[1], A.p[0], acc2, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A.p[0], A.p[0], acc, 0, 0, 0);
+}
+
 // Operands straight from global memory into registers, no LDS: a lane's fragment is
 // rows kw .. kw+7 of one column, eight buffer loads that differ only in their SGPR
 // offset (r * ld * 4 bytes), so the addressing costs no VALU; the buffer's record
@@ -2194,9 +2204,9 @@ __global__ __launch_bounds__(XS_THREADS, 1) void kfac_factor_conv_x3s(FactorArgs
   }
   __shared__ int ftab[32];  // block row -> factor row / column (the epilogue's stores)
   if (tid < 32) ftab[tid] = fme;
-  floatx16 acc;
+  floatx16 acc, acc2;  // (hh + mm, and the cross products' half: x3_four)
 #pragma unroll
-  for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+  for (int v = 0; v < 16; ++v) acc[v] = acc2[v] = 0.f;
   // group q = 2t + hi of k-step t: output row q / g8, columns 8 (q mod g8) .. + 7.  A
   // wave's k-steps t = gw + 4 j are groups q0 + 8 j, and g8 divides 8, so its fragment
   // addresses are a0 + j delta (no per-k-step index math; a table read in LDS, which the
@@ -2229,19 +2239,19 @@ __global__ __launch_bounds__(XS_THREADS, 1) void kfac_factor_conv_x3s(FactorArgs
     for (; j + 3 <= Jn; j += 3) {
       load(buf, min(j + 2, last), k2);
       __builtin_amdgcn_sched_barrier(0);
-      x3_six(acc, k0, k0);
+      x3_four(acc, acc2, k0);
       __builtin_amdgcn_sched_barrier(0);
       load(buf, min(j + 3, last), k0);
       __builtin_amdgcn_sched_barrier(0);
-      x3_six(acc, k1, k1);
+      x3_four(acc, acc2, k1);
       __builtin_amdgcn_sched_barrier(0);
       load(buf, min(j + 4, last), k1);
       __builtin_amdgcn_sched_barrier(0);
-      x3_six(acc, k2, k2);
+      x3_four(acc, acc2, k2);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (j < Jn) x3_six(acc, k0, k0);
-    if (j + 1 < Jn) x3_six(acc, k1, k1);
+    if (j < Jn) x3_four(acc, acc2, k0);
+    if (j + 1 < Jn) x3_four(acc, acc2, k1);
   };
 
   // phase i: group i % 2 multiplies image i, the other group builds image i + 1, then
@@ -2285,16 +2295,31 @@ __global__ __launch_bounds__(XS_THREADS, 1) void kfac_factor_conv_x3s(FactorArgs
       phase_mma(i + 1);
     }
   }
-  // the 8 waves' partial sums, summed in wave order by wave 0 (deterministic)
+  // the 8 waves' partial sums, summed in wave order by wave 0 (deterministic); then
+  // acc + acc2 + acc2^T, the transpose through LDS (wave 0's LDS operations complete in
+  // order: its writes are read back with no barrier)
   float* red = reinterpret_cast<float*>(cxs);
+  float* red2 = red + (XS_WAVES - 1) * 16 * 64;
   if (wave > 0)
 #pragma unroll
-    for (int v = 0; v < 16; ++v) red[((wave - 1) * 16 + v) * 64 + lane] = acc[v];
+    for (int v = 0; v < 16; ++v) {
+      red[((wave - 1) * 16 + v) * 64 + lane] = acc[v];
+      red2[((wave - 1) * 16 + v) * 64 + lane] = acc2[v];
+    }
   __syncthreads();
   if (wave > 0) return;
   for (int w = 0; w < XS_WAVES - 1; ++w)
 #pragma unroll
-    for (int v = 0; v < 16; ++v) acc[v] += red[(w * 16 + v) * 64 + lane];
+    for (int v = 0; v < 16; ++v) {
+      acc[v] += red[(w * 16 + v) * 64 + lane];
+      acc2[v] += red2[(w * 16 + v) * 64 + lane];
+    }
+  float* tr = red2 + (XS_WAVES - 1) * 16 * 64;  // 32 x 33
+#pragma unroll
+  for (int v = 0; v < 16; ++v) tr[acc_row(v, lane) * 33 + (lane & 31)] = acc2[v];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc[v] += acc2[v] + tr[(lane & 31) * 33 + acc_row(v, lane)];
   float* o = J.slab + (size_t)split * TILE * TILE;  // block (0, 0) of slab tile 0
   const int fc = ftab[lane & 31];
   put_partial(J, acc, [&](int v) { return &o[ftab[acc_row(v, lane)] * TILE + fc]; });
@@ -2338,21 +2363,32 @@ constexpr int XF_BUF = 3 * XF_PART;       // one copy buffer (hi, mid, lo parts)
 constexpr int XF_REC = 2 * XF_BUF;        // build-slot records: [slot i][group thread] u32x2
 constexpr int XF_TBL = XF_REC + XF_SP * XF_GROUP * 8;  // copy bases: u16 [c][kj][v] (v < 2)
 constexpr int XF_LDS = XF_TBL + XF_CB * 2;  // (a 29 KB inversion workgroup still fits beside it)
-static_assert(XF_LDS <= 134144 && XF_BUF >= XF_GW * XF_BPW * 16 * 64 * 4 / 2, "x3f LDS");
+static_assert(XF_LDS <= 134144, "x3f LDS");
 
 // A multiplying wave's blocks as pairs (a, b) of indices into its fragment set F: block
-// (F[a], F[b]).  Assignments (conv_x3f_geom): 5 block rows (n = 129..160): waves take
-// patterns 0-3 with F = {0,1,4}, {0,1,2,3}, {0,1,2,4}, {2,3,4}; 4 block rows (97..128):
-// patterns 4-6 with F = {0,1}, {0,1,2}, {0,1,2,3} and an idle wave.
+// (F[a], F[b]); a diagonal block (a = b) takes x3_four (four MFMAs and a transposed
+// half, acc2) instead of six.  Assignments (conv_x3f_geom), from an exact-cover search
+// over the lower triangle's blocks (<= 4 blocks and <= 4 fragments per wave, block order
+// maximizing the MFMAs between a fragment's reload and its next use):
+//   5 block rows (n = 129..160): F = {0,1,2,3} (0,0) (1,1) (3,2) -- 14 MFMAs per k-step;
+//     {0,1,2,4} (2,2) (2,0) (1,0) (4,1); {1,2,3,4} (2,1) (3,1) (4,3) (4,4);
+//     {0,2,3,4} (3,3) (3,0) (4,0) (4,2) -- 22 each (six-product diagonals: 24 on the
+//     busiest wave), >= 8 MFMAs of slack per reload (was 6);
+//   4 block rows (97..128): F = {0,1,2,3} for all: (0,0) (1,1) (3,2); (1,0) (2,2) (3,3);
+//     (2,0) (3,1); (2,1) (3,0) -- 14, 14, 12, 12.
 struct XfPat {
   int a[4], b[4], n;
 };
 constexpr XfPat XF_PAT[] = {
-    {{0, 1, 1, 2}, {0, 0, 1, 2}, 4}, {{2, 2, 3, 3}, {0, 1, 0, 1}, 4}, {{3, 3, 3, 2}, {0, 1, 2, 2}, 4},
-    {{1, 1, 2, 0}, {0, 1, 1, 0}, 3}, {{0, 1, 1, 0}, {0, 0, 1, 0}, 3}, {{2, 2, 2, 0}, {0, 1, 2, 0}, 3},
-    {{3, 3, 3, 3}, {0, 1, 2, 3}, 4}};
+    {{0, 1, 3, 0}, {0, 1, 2, 0}, 3}, {{2, 2, 1, 3}, {2, 0, 0, 1}, 4}, {{1, 2, 3, 3}, {0, 0, 2, 3}, 4},
+    {{2, 2, 3, 3}, {2, 0, 0, 1}, 4}, {{1, 2, 3, 0}, {0, 2, 3, 0}, 3}, {{2, 3, 0, 0}, {0, 1, 0, 0}, 2},
+    {{2, 3, 0, 0}, {1, 0, 0, 0}, 2}};
 constexpr int XF_NPAT = sizeof(XF_PAT) / sizeof(XF_PAT[0]);
 constexpr int XF_PAT_IDLE = 15;
+constexpr int XF_D2 = 2;  // diagonal blocks per wave at most (acc2 sets)
+// (the epilogue's exchange -- 4 waves x 6 sets of 16 x 64 floats -- and 4 transpose tiles
+// fit the two copy buffers)
+static_assert(2 * XF_BUF >= (XF_GW * (XF_BPW + XF_D2) * 16 * 64 + XF_GW * 32 * 33) * 4, "x3f epilogue LDS");
 __host__ __device__ constexpr int xf_pat_frags(const XfPat& p) {
   int m = 0;
   for (int s = 0; s < p.n; ++s) m = std::max(m, std::max(p.a[s], p.b[s]) + 1);
@@ -2363,6 +2399,11 @@ __host__ __device__ constexpr int xf_pat_last_use(const XfPat& p, int q) {
   for (int s = 0; s < p.n; ++s)
     if (p.a[s] == q || p.b[s] == q) l = s;
   return l;
+}
+__host__ __device__ constexpr int xf_pat_diag(const XfPat& p, int s) {  // acc2 set of block s
+  int d = 0;
+  for (int t = 0; t < s; ++t) d += p.a[t] == p.b[t];
+  return d;
 }
 __host__ __device__ inline int xf_pat_blocks(int pat) { return XF_PAT[pat].n; }
 __host__ __device__ inline int xf_pat_a(int pat, int s) { return XF_PAT[pat].a[s]; }
@@ -2509,11 +2550,15 @@ __global__ __launch_bounds__(XF_THREADS, 1) void kfac_factor_conv_x3f(FactorArgs
   int offF[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) offF[q] = row_off(32 * ((wcode >> (4 + 3 * q)) & 7) + m) + 16 * hh;
-  floatx16 acc[XF_BPW];
+  floatx16 acc[XF_BPW], acc2[XF_D2];
 #pragma unroll
   for (int i = 0; i < XF_BPW; ++i)
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[i][v] = 0.f;
+#pragma unroll
+  for (int i = 0; i < XF_D2; ++i)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc2[i][v] = 0.f;
   // the last k-step's positions past L (L even): fragments masked by dword
   const int nks = cg.xf_nks, last = nks - 1;
   const int vc = min(max(cg.L - (16 * last + 8 * hh), 0), 8);
@@ -2560,10 +2605,14 @@ __global__ __launch_bounds__(XF_THREADS, 1) void kfac_factor_conv_x3f(FactorArgs
 #pragma unroll
       for (int q = 0; q < NF; ++q)
         if (xf_pat_last_use(P, q) == s2) load(0, q);
+    auto prod = [&](int s2) __attribute__((always_inline)) {  // (s2: unrolled constant)
+      if (P.a[s2] == P.b[s2]) x3_four(acc[s2], acc2[xf_pat_diag(P, s2)], F[P.a[s2]]);
+      else x3_six(acc[s2], F[P.a[s2]], F[P.b[s2]]);
+    };
     for (int t = 0; t < last; ++t) {
 #pragma unroll
       for (int s2 = 0; s2 < P.n; ++s2) {
-        x3_six(acc[s2], F[P.a[s2]], F[P.b[s2]]);
+        prod(s2);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < NF; ++q)
@@ -2573,7 +2622,7 @@ __global__ __launch_bounds__(XF_THREADS, 1) void kfac_factor_conv_x3f(FactorArgs
     }
     mask_all(F, NF);
 #pragma unroll
-    for (int s2 = 0; s2 < P.n; ++s2) x3_six(acc[s2], F[P.a[s2]], F[P.b[s2]]);
+    for (int s2 = 0; s2 < P.n; ++s2) prod(s2);
   };
   auto mma = [&](const char* buf) __attribute__((always_inline)) {
     switch (pat) {
@@ -2632,9 +2681,12 @@ __global__ __launch_bounds__(XF_THREADS, 1) void kfac_factor_conv_x3f(FactorArgs
       phase_mma(i + 1);
     }
   }
-  // group 1's partial sums added to group 0's (fixed order), then stored by group 0
-  // (group 0's accumulator reads in flight across the exchange)
+  // group 1's partial sums added to group 0's (fixed order), then the diagonal blocks'
+  // acc + acc2 + acc2^T (the transpose through a per-wave LDS tile: a wave's LDS
+  // operations complete in order), stored by group 0 (its accumulator reads in flight
+  // across the exchange)
   float* red = reinterpret_cast<float*>(cxf);
+  constexpr int XF_SETS = XF_BPW + XF_D2;
   const int nblk = pat < XF_NPAT ? xf_pat_blocks(pat) : 0;
   auto at = [&](int i, int v) __attribute__((always_inline)) {
     const int bi = (wcode >> (4 + 3 * xf_pat_a(pat, i))) & 7, bj = (wcode >> (4 + 3 * xf_pat_b(pat, i))) & 7;
@@ -2646,19 +2698,39 @@ __global__ __launch_bounds__(XF_THREADS, 1) void kfac_factor_conv_x3f(FactorArgs
   float old[XF_BPW][16];
   if (grp == 1) {
 #pragma unroll
-    for (int i = 0; i < XF_BPW; ++i)
+    for (int i = 0; i < XF_SETS; ++i)
 #pragma unroll
-      for (int v = 0; v < 16; ++v) red[((gw * XF_BPW + i) * 16 + v) * 64 + lane] = acc[i][v];
+      for (int v = 0; v < 16; ++v)
+        red[((gw * XF_SETS + i) * 16 + v) * 64 + lane] = i < XF_BPW ? acc[i][v] : acc2[i - XF_BPW][v];
   } else {
     load_partials(J, nblk, old, at);
   }
   __syncthreads();
   if (grp == 1) return;
 #pragma unroll
+  for (int i = 0; i < XF_BPW; ++i)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[i][v] += red[((gw * XF_SETS + i) * 16 + v) * 64 + lane];
+#pragma unroll
+  for (int i = 0; i < XF_D2; ++i)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc2[i][v] += red[((gw * XF_SETS + XF_BPW + i) * 16 + v) * 64 + lane];
+  float* tr = red + XF_GW * XF_SETS * 16 * 64 + gw * 32 * 33;  // this wave's 32 x 33 tile
+  int d = 0;
+#pragma unroll
   for (int i = 0; i < XF_BPW; ++i) {
     if (i >= nblk) break;
+    if (xf_pat_a(pat, i) != xf_pat_b(pat, i)) continue;
+    floatx16 y = acc2[0];
 #pragma unroll
-    for (int v = 0; v < 16; ++v) acc[i][v] += red[((gw * XF_BPW + i) * 16 + v) * 64 + lane];
+    for (int v = 0; v < 16; ++v) y[v] = d ? acc2[1][v] : y[v];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) tr[acc_row(v, lane) * 33 + (lane & 31)] = y[v];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[i][v] += y[v] + tr[(lane & 31) * 33 + acc_row(v, lane)];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the tile's reads before its next writes)
+    ++d;
   }
   put_partials(J, nblk, acc, old, at);
 }
@@ -2911,8 +2983,8 @@ static bool conv_x3s_geom(const kfac_operand& o, ConvGeom& g) {
   g.sh = o.sh;
   g.sw = o.sw;
   g.ones = ones;
-  // (the epilogue's partial-sum exchange: 7 waves x 16 x 64 floats)
-  g.ldsb = (int)std::max<int64_t>(best_b, (XS_WAVES - 1) * 16 * 64 * 4);
+  // (the epilogue's partial-sum exchange: 2 x 7 waves x 16 x 64 floats, a 32 x 33 transpose)
+  g.ldsb = (int)std::max<int64_t>(best_b, 2 * (XS_WAVES - 1) * 16 * 64 * 4 + 32 * 33 * 4);
   g.nb = 1;
   g.nq = 1;
   g.mode = 5;
@@ -3062,15 +3134,15 @@ static bool conv_x3f_geom_new(const kfac_operand& o, ConvGeom& g) {
     return c;
   };
   if (nb == 5) {
-    g.xf_wave[0] = wave_code(0, {0, 1, 4});
-    g.xf_wave[1] = wave_code(1, {0, 1, 2, 3});
-    g.xf_wave[2] = wave_code(2, {0, 1, 2, 4});
-    g.xf_wave[3] = wave_code(3, {2, 3, 4});
+    g.xf_wave[0] = wave_code(0, {0, 1, 2, 3});
+    g.xf_wave[1] = wave_code(1, {0, 1, 2, 4});
+    g.xf_wave[2] = wave_code(2, {1, 2, 3, 4});
+    g.xf_wave[3] = wave_code(3, {0, 2, 3, 4});
   } else {
-    g.xf_wave[0] = wave_code(4, {0, 1});
-    g.xf_wave[1] = wave_code(5, {0, 1, 2});
-    g.xf_wave[2] = wave_code(6, {0, 1, 2, 3});
-    g.xf_wave[3] = XF_PAT_IDLE;
+    g.xf_wave[0] = wave_code(0, {0, 1, 2, 3});
+    g.xf_wave[1] = wave_code(4, {0, 1, 2, 3});
+    g.xf_wave[2] = wave_code(5, {0, 1, 2, 3});
+    g.xf_wave[3] = wave_code(6, {0, 1, 2, 3});
   }
   g.xs_hp = hp;
   g.xs_wp2 = wp2;
