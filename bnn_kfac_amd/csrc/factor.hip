@@ -3493,8 +3493,10 @@ static bool syrk3_group(const kfac_factor_job* jobs, int njobs) {
 // fp32-MFMA kfac_factor_tiles).  MNIST MLP, same box, 2 reps: 1.21-1.23e8 vs
 // 1.01e8 img/s, 81-82 vs 108 us per launch, the inversion beside the pass 0.41 vs
 // 0.61 ms (2 SYRK waves per SIMD instead of 4).  Groups whose largest factor has
-// n < 512 keep the fp32 kernel (LeNet-5's fully connected factors, n <= 401: 1.34e7
-// vs 1.39e7 img/s with x3).
+// n < 256 keep the fp32 kernel.  LeNet-5's fully connected factors (n <= 401) measured
+// 1.34e7 vs 1.39e7 img/s with x3 in round 5; with round 6's conv kernels the pass is
+// 2.01-2.02 vs 2.06 ms with x3 (0.26 vs 0.31 ms of fc factors, 3 reps alternating,
+// `profiles/r06z13/`), so the threshold moved from 512 to 256.
 static int tiles_x3_mode() { return knobs().tiles_x3; }
 
 static bool tiles_x3_group(const kfac_factor_job* jobs, int njobs) {
@@ -3508,7 +3510,7 @@ static bool tiles_x3_group(const kfac_factor_job* jobs, int njobs) {
     if (n > 32 && jobs[i].x.rows * jobs[i].x.ld * (int64_t)sizeof(float) >= ((int64_t)1 << 31)) return false;
     nmax = std::max(nmax, n);
   }
-  return nmax >= (tiles_x3_mode() == 1 ? 33 : 512);
+  return nmax >= (tiles_x3_mode() == 1 ? 33 : 256);
 }
 
 static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,

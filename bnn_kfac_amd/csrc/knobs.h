@@ -11,7 +11,7 @@ struct Knobs {
   // factor-product kernel selection (-1 auto, 0 off, 1 forced): fixed at load, since a
   // pass's accumulator plan and its launches must agree on the kernel
   int syrk3;       // KFAC_SYRK3: kfac_factor_syrk3 for row-major groups (auto: largest n >= 2048)
-  int tiles_x3;    // KFAC_TILES_X3: kfac_factor_tiles_x3 (auto: largest n >= 512)
+  int tiles_x3;    // KFAC_TILES_X3: kfac_factor_tiles_x3 (auto: largest n >= 256)
   int conv_small;  // KFAC_CONV_SMALL: channel factors with n <= 8 on kfac_factor_channel_small (1)
   int conv_k;      // KFAC_CONV_K: images per conv task (0: the planner's)
   int conv_x3;     // KFAC_CONV_X3: im2col factors with n > 32 on kfac_factor_conv_x3 (bf16x3) (1)
