@@ -322,7 +322,7 @@ def verify_parity(kfac, net, specs, recs, batch, images, world, rank, device, sy
 # the factor-product kernel families (profile slots of the library, named as rocprofv3
 # names them) that compute each fp32 product as six bf16 MFMA products
 BF16X3_KERNELS = ("kfac_factor_tiles_x3", "kfac_factor_syrk3", "kfac_factor_conv_x3", "kfac_factor_conv_x3s",
-                  "kfac_factor_conv_x3f")
+                  "kfac_factor_conv_x3f", "kfac_factor_channel_x3")
 
 
 def load_traffic(config):

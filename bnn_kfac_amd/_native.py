@@ -24,14 +24,14 @@ OUT_INV_CHOL, OUT_INVERSE = 0, 1
 TRI_SYMMETRIC, TRI_LOWER = 0, 1
 (PROF_FACTOR_TILES, PROF_FACTOR_REDUCE, PROF_INVERT, PROF_QUAD_TILES, PROF_FACTOR_SYRK3,
  PROF_FACTOR_X3, PROF_FACTOR_CONV, PROF_FACTOR_CHANNEL_SMALL, PROF_SYEV, PROF_FACTOR_CONV_X3,
- PROF_FACTOR_CONV_X3S, PROF_FACTOR_CONV_X3F) = range(12)
+ PROF_FACTOR_CONV_X3S, PROF_FACTOR_CONV_X3F, PROF_FACTOR_CHANNEL_X3) = range(13)
 # profile slot -> the kernel family rocprofv3 names (kfac_prof_id, include/kfac_hip.h; the
 # fp32 SYRK is the template kfac_factor_tiles_t<...>, named without the _t as in profiles/)
 PROF_FACTOR_KERNELS = {PROF_FACTOR_TILES: "kfac_factor_tiles", PROF_FACTOR_SYRK3: "kfac_factor_syrk3",
                        PROF_FACTOR_X3: "kfac_factor_tiles_x3", PROF_FACTOR_CONV: "kfac_factor_conv",
                        PROF_FACTOR_CHANNEL_SMALL: "kfac_factor_channel_small",
                        PROF_FACTOR_CONV_X3: "kfac_factor_conv_x3", PROF_FACTOR_CONV_X3S: "kfac_factor_conv_x3s",
-                       PROF_FACTOR_CONV_X3F: "kfac_factor_conv_x3f"}
+                       PROF_FACTOR_CONV_X3F: "kfac_factor_conv_x3f", PROF_FACTOR_CHANNEL_X3: "kfac_factor_channel_x3"}
 
 c_i32, c_i64, c_f32, c_f64, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_void_p
 

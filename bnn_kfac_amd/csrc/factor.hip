@@ -2384,7 +2384,6 @@ constexpr XfPat XF_PAT[] = {
     {{2, 2, 3, 3}, {2, 0, 0, 1}, 4}, {{1, 2, 3, 0}, {0, 2, 3, 0}, 3}, {{2, 3, 0, 0}, {0, 1, 0, 0}, 2},
     {{2, 3, 0, 0}, {1, 0, 0, 0}, 2}};
 constexpr int XF_NPAT = sizeof(XF_PAT) / sizeof(XF_PAT[0]);
-constexpr int XF_PAT_IDLE = 15;
 constexpr int XF_D2 = 2;  // diagonal blocks per wave at most (acc2 sets)
 // (the epilogue's exchange -- 4 waves x 6 sets of 16 x 64 floats -- and 4 transpose tiles
 // fit the two copy buffers)
@@ -2633,7 +2632,7 @@ __global__ __launch_bounds__(XF_THREADS, 1) void kfac_factor_conv_x3f(FactorArgs
       case 4: mma_pat(buf, std::integral_constant<int, 4>{}); break;
       case 5: mma_pat(buf, std::integral_constant<int, 5>{}); break;
       case 6: mma_pat(buf, std::integral_constant<int, 6>{}); break;
-      default: break;  // (XF_PAT_IDLE: no blocks)
+      default: break;
     }
   };
   // phases as mode 5: group i % 2 multiplies image i, the other builds image i + 1 and
@@ -2825,6 +2824,101 @@ __global__ __launch_bounds__(NTHREADS) void kfac_factor_channel_small(FactorArgs
       *at2 = v;
     }
   }
+}
+
+// Channel-major factors with 8 < n <= 32 (LeNet-5's conv2 G: 16 channels x 100
+// positions per image) in bf16x3, fragments straight from HBM: a channel's positions
+// are contiguous, so a lane's fragment -- 8 consecutive positions of one channel -- is
+// two float4 loads, split in registers (x3_split8); one 32 x 32 diagonal block, four
+// MFMAs per 16 positions (x3_four).  Each wave takes whole images (images w, w + 4, ..
+// of the task), its k-steps flattened over them with XC_D k-steps of loads in flight;
+// the 4 waves' sums meet in LDS in wave order, then acc + acc2 + acc2^T.  (It replaces
+// the LDS-staged fp32 kernel there: an HBM stream at 2.2 TB/s.)
+constexpr int XC_D = 4;  // k-steps of loads in flight per wave
+__global__ __launch_bounds__(NTHREADS) void kfac_factor_channel_x3(FactorArgs args, ConvGeom cg) {
+  __shared__ float red[2 * (NTHREADS / 64 - 1)][16][64];
+  __shared__ float tr[32][33];
+  const int task = xcd_task(blockIdx.x, gridDim.x);
+  int jx = 0;
+  while (jx + 1 < args.njobs && task >= args.task_end[jx]) ++jx;
+  const FactorJobDev& J = args.job[jx];
+  const OpDev& op = J.x;
+  const int split = task - J.task_begin;  // one unit: task = split
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = op.cols, L = (int)op.L, m = lane & 31, hh = lane >> 5;
+  const int64_t b0 = (int64_t)split * cg.B / J.splits, b1 = (int64_t)(split + 1) * cg.B / J.splits;
+  const int nks = (L + 15) / 16;
+  const int nimg = b1 - b0 > wave ? (int)((b1 - b0 - wave + 3) / 4) : 0;
+  const int total = nimg * nks;  // this wave's k-steps
+  // cursor of the next k-step to load: image j of the wave, k-step t; its channel row
+  const float* rowp = nullptr;
+  int j = 0, t = 0;
+  auto image_row = [&](int jj) __attribute__((always_inline)) {
+    const uint32_t ab = (uint32_t)(b0 + wave + 4 * (int64_t)jj), seg = ab / (uint32_t)cg.bseg;
+    return seg_base(J, args.segs, (int)seg) + (int64_t)(ab - seg * cg.bseg) * op.sB + (int64_t)min(m, n - 1) * L;
+  };
+  if (total > 0) rowp = image_row(0);
+  auto load = [&](float (&x)[8]) __attribute__((always_inline)) {
+    const int p = 16 * t + 8 * hh;
+    const bool r0 = m < n && p < L, r1 = m < n && p + 4 < L;
+    const floatx4 lo = r0 ? *reinterpret_cast<const floatx4*>(rowp + p) : floatx4{0.f, 0.f, 0.f, 0.f};
+    const floatx4 hi = r1 ? *reinterpret_cast<const floatx4*>(rowp + p + 4) : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      x[e] = lo[e];
+      x[4 + e] = hi[e];
+    }
+    if (++t == nks) {
+      t = 0;
+      if (++j < nimg) rowp = image_row(j);
+      else j = nimg;
+    }
+  };
+  floatx16 acc, acc2;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc[v] = acc2[v] = 0.f;
+  // ring of XC_D k-steps: step s multiplies slot s % XC_D, then reloads it for s + XC_D
+  // (unconditionally: past the wave's last k-step the cursor re-reads its last image,
+  // unused -- a conditional load made every wait vmcnt(0))
+  if (total > 0) {
+    float x[XC_D][8];
+#pragma unroll
+    for (int d = 0; d < XC_D; ++d) load(x[d]);
+    int s = 0;
+    for (; s + XC_D <= total; s += XC_D) {
+#pragma unroll
+      for (int d = 0; d < XC_D; ++d) {
+        const X3Frag f = x3_split8(x[d]);
+        load(x[d]);
+        x3_four(acc, acc2, f);
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < XC_D; ++d)
+      if (s + d < total) x3_four(acc, acc2, x3_split8(x[d]));
+  }
+  // the 4 waves' sums in wave order (deterministic), then acc + acc2 + acc2^T
+  if (wave > 0)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      red[2 * (wave - 1)][v][lane] = acc[v];
+      red[2 * (wave - 1) + 1][v][lane] = acc2[v];
+    }
+  __syncthreads();
+  if (wave > 0) return;
+  for (int w = 0; w < NTHREADS / 64 - 1; ++w)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      acc[v] += red[2 * w][v][lane];
+      acc2[v] += red[2 * w + 1][v][lane];
+    }
+#pragma unroll
+  for (int v = 0; v < 16; ++v) tr[acc_row(v, lane)][m] = acc2[v];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc[v] += acc2[v] + tr[m][acc_row(v, lane)];
+  float* out = J.slab + (size_t)split * TILE * TILE;  // block (0, 0) of slab tile 0
+  put_partial(J, acc, [&](int v) { return &out[acc_row(v, lane) * TILE + m]; });
 }
 
 // KFAC_CONV_SMALL=0: channel factors with n <= 8 on the MFMA kernel (A/B checks)
@@ -3252,6 +3346,11 @@ constexpr int KFAC_CONV_NARROW32 = 3;  // n in 17..32: 3 = three 16x16 blocks, 1
   g.nq = nb * (nb + 1) / 2;
   g.units = g.mode ? 1 : (int)cdiv(g.nq, 4 * CONV_CB);
   g.lds = (int)lds;
+  // mode 8 (kfac_factor_channel_x3): CHANNEL factors with 8 < n <= 32, bf16x3 from HBM
+  if (o.layout == KFAC_CHANNEL && n > 8 && n <= 32 && knobs().conv_x3) {
+    g.mode = 8;
+    g.units = 1;
+  }
   return true;
 }
 
@@ -3289,6 +3388,10 @@ static void launch_conv(const FactorArgs& args, const ConvGeom& g, int tasks, hi
                   : bpw == 2 ? launch_conv_x3<2>(args, g, tasks, stream)
                              : launch_conv_x3<3>(args, g, tasks, stream);
     (void)ok;  // (a failed attribute surfaces as the launch error below)
+    return;
+  }
+  if (g.mode == 8) {
+    hipLaunchKernelGGL(kfac_factor_channel_x3, dim3(tasks), dim3(NTHREADS), 0, stream, args, g);
     return;
   }
   if (LAYOUT == KFAC_CHANNEL && channel_small(g)) {
@@ -3608,8 +3711,8 @@ static void plan_jobs(const kfac_factor_job* jobs, int njobs, Plan* plans,
       // larger cost there: conv1 G 15.7 / 12.4 / 13.2 us at k = 1 / 2 / 4)
       const bool small = jobs[i].x.layout == KFAC_CHANNEL && channel_small(cg);
       // (mode-0 instances are compiled for KFAC_CONV_OCC resident workgroups per CU;
-      // modes 4-6 run one 512-thread workgroup per CU)
-      const int64_t cslots = cg.mode == 0 ? (int64_t)KFAC_CONV_OCC * 256 : cg.mode >= 4 ? 256 : slots;
+      // modes 4-6 run one 512-thread workgroup per CU, mode 8 four of 256)
+      const int64_t cslots = cg.mode == 0 ? (int64_t)KFAC_CONV_OCC * 256 : (cg.mode >= 4 && cg.mode <= 6) ? 256 : slots;
       // (a multi-batch launch -- thousands of images -- amortizes that reduction: the n <= 8
       // kernel then takes 4 workgroups per CU, twice the loads in flight of 2)
       const bool halve = small && cg.B <= 8 * cslots;
@@ -3757,6 +3860,7 @@ static int factor_group(const kfac_factor_job* jobs, int njobs, char* ws, size_t
                      : !staged ? KFAC_PROF_FACTOR_TILES
                      : (jobs[0].x.layout == KFAC_CHANNEL && channel_small(cg))
                          ? KFAC_PROF_FACTOR_CHANNEL_SMALL
+                     : cg.mode == 8 ? KFAC_PROF_FACTOR_CHANNEL_X3
                      : cg.mode == 6 ? KFAC_PROF_FACTOR_CONV_X3F
                      : cg.mode == 5 ? KFAC_PROF_FACTOR_CONV_X3S
                      : cg.mode == 4 ? KFAC_PROF_FACTOR_CONV_X3 : KFAC_PROF_FACTOR_CONV;

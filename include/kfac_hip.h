@@ -339,7 +339,7 @@ KFAC_API int kfac_tri_unpack(const kfac_tri_job* jobs, int njobs, const float* p
  *   11 kfac_factor_conv_x3f (stride-1 im2col factors with 32 < n <= 160, bf16x3 from
  *     flattened column copies).
  * kfac_profile_read syncs the recorded events.  kfac_profile_read_work also
- * returns the slot's algorithmic work: `work` = flops, for the factor slots (0, 4-7, 9-11)
+ * returns the slot's algorithmic work: `work` = flops, for the factor slots (0, 4-7, 9-12)
  * sum_jobs K_rows * n (n + 1) (lower triangle incl. the diagonal, 2 flops per
  * product; curvatures.py:341-356); `bytes` = HBM bytes, for the factor slots each
  * operand read once (rows x cols x 4; an im2col operand: its images), for the syev
@@ -348,7 +348,7 @@ enum kfac_prof_id { KFAC_PROF_FACTOR_TILES = 0, KFAC_PROF_FACTOR_REDUCE = 1, KFA
                     KFAC_PROF_QUAD_TILES = 3, KFAC_PROF_FACTOR_SYRK3 = 4, KFAC_PROF_FACTOR_X3 = 5,
                     KFAC_PROF_FACTOR_CONV = 6, KFAC_PROF_FACTOR_CHANNEL_SMALL = 7, KFAC_PROF_SYEV = 8,
                     KFAC_PROF_FACTOR_CONV_X3 = 9, KFAC_PROF_FACTOR_CONV_X3S = 10,
-                    KFAC_PROF_FACTOR_CONV_X3F = 11, KFAC_PROF_COUNT = 12 };
+                    KFAC_PROF_FACTOR_CONV_X3F = 11, KFAC_PROF_FACTOR_CHANNEL_X3 = 12, KFAC_PROF_COUNT = 13 };
 KFAC_API int kfac_profile_enable(int on);
 KFAC_API int kfac_profile_read(int id, double* total_ms, int64_t* launches);
 KFAC_API int kfac_profile_read_work(int id, double* total_ms, int64_t* launches, double* work,

@@ -33,6 +33,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FETCH_SCALE = 2.0
 FACTOR_FAMILIES = ("kfac_factor_tiles", "kfac_factor_tiles_x3", "kfac_factor_syrk3", "kfac_factor_conv",
                    "kfac_factor_conv_x3", "kfac_factor_conv_x3s", "kfac_factor_conv_x3f", "kfac_factor_channel_small",
+                   "kfac_factor_channel_x3",
                    "kfac_factor_reduce")
 
 

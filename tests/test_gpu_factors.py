@@ -198,6 +198,31 @@ def test_conv_shapes_vs_oracle(hip_device, spec):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("B,cout,hw", [(9000, 16, 10), (300, 11, 14), (40, 32, 6), (5, 9, 22)])
+def test_channel_x3(hip_device, B, cout, hw):
+    """G of a conv layer with 8 < n <= 32 on kfac_factor_channel_x3 (bf16x3 fragments
+    straight from HBM, one diagonal block in four MFMAs): LeNet-5's conv2 G over 9,000
+    images in one launch, and n = 11 / 32 / 9 over 196, 36 and 484 positions (a last
+    k-step with 4 positions: half a float4 pair), fewer images than waves."""
+    from bnn_kfac_amd import _native as N
+    from bnn_kfac_amd.curvatures import KFAC
+    rng = np.random.default_rng(B + cout)
+    conv = nn.Conv2d(3, cout, 3, bias=True).to(hip_device)
+    x = rng.random((B, 3, hw + 2, hw + 2), dtype=np.float32)
+    gr = rng.standard_normal((B, cout, hw, hw), dtype=np.float32)
+    kfac = KFAC(conv)
+    kfac.record[conv] = [_t(x, hip_device), _t(gr, hip_device)]
+    N.profile_reset()
+    N.profile_enable(True)
+    kfac.update(batch_size=B)
+    torch.cuda.synchronize()
+    N.profile_enable(False)
+    assert N.profile_read(N.PROF_FACTOR_CHANNEL_X3)[1] == 1
+    _, G = kfac.state[conv]
+    np.testing.assert_allclose(G.cpu().numpy(), O.grad_factor(gr, np.float64), **FT)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cout", [6, 7])
 def test_channel_small_large_launch(hip_device, cout):
     """G of a conv layer over 9,000 images in one launch (the n <= 8 register-triangle
