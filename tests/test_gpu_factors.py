@@ -223,6 +223,25 @@ def test_channel_x3(hip_device, B, cout, hw):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cout", [6, 16])
+def test_channel_operand_with_ones(hip_device, cout):
+    """A CHANNEL operand with a ones column (legal in the C ABI, unused by the hooks):
+    F = [G | 1]^T [G | 1] stays on the staged kernel, which has the ones plane."""
+    from bnn_kfac_amd import _native as N
+    B, L = 64, 36
+    rng = np.random.default_rng(cout)
+    g = rng.standard_normal((B, cout, L), dtype=np.float32)
+    op = N.channel_operand(_t(g.reshape(B, cout, 6, 6), hip_device))
+    op.has_ones = 1
+    n = cout + 1
+    F = torch.zeros((n, n), device=hip_device)
+    N.factor_update([N.factor_job(op, F, 1.0, 0.0)], hip_device)
+    torch.cuda.synchronize()
+    X = np.concatenate([g.transpose(0, 2, 1).reshape(-1, cout), np.ones((B * L, 1), np.float32)], 1)
+    np.testing.assert_allclose(F.cpu().numpy(), X.T.astype(np.float64) @ X, **FT)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cout", [6, 7])
 def test_channel_small_large_launch(hip_device, cout):
     """G of a conv layer over 9,000 images in one launch (the n <= 8 register-triangle
