@@ -2926,9 +2926,7 @@ static bool conv_small_off() { return !knobs().conv_small; }
 // the register-triangle kernel takes channel factors with n <= 8 (an n = 16 instance --
 // 136 sums per thread, 256 VGPRs -- ran LeNet-5's conv2 G at 0.63 ms per pass against
 // 0.17 on the MFMA kernel, `profiles/r06z10/`)
-// (a CHANNEL operand with a ones column -- legal, unused by the hooks -- keeps the
-// staged kernel, which has the ones plane)
-static bool channel_small(const ConvGeom& g) { return !conv_small_off() && g.n <= 8 && g.ones < 0; }
+static bool channel_small(const ConvGeom& g) { return !conv_small_off() && g.n <= 8; }
 
 // Geometry of a conv job on the LDS-staged kernel; false: the job takes the
 // register-staged path (images too large, channel blocks not float4-shaped, or an
@@ -3272,6 +3270,9 @@ static bool conv_geom(const kfac_factor_job& j, ConvGeom& g) {
   if ((o.layout != KFAC_PATCH && o.layout != KFAC_CHANNEL) || o.rows <= 0 || o.L <= 0 ||
       o.rows % o.L != 0 || nseg * (o.rows / o.L) > (1 << 30))
     return false;
+  // (a CHANNEL operand with a ones column -- legal, unused by the hooks -- takes the
+  // unstaged kernel: the channel kernels have no ones row)
+  if (o.layout == KFAC_CHANNEL && o.has_ones) return false;
   const int n = o.cols + (o.has_ones ? 1 : 0);
   g = ConvGeom{};
   g.n = n;
@@ -3350,7 +3351,7 @@ constexpr int KFAC_CONV_NARROW32 = 3;  // n in 17..32: 3 = three 16x16 blocks, 1
   g.units = g.mode ? 1 : (int)cdiv(g.nq, 4 * CONV_CB);
   g.lds = (int)lds;
   // mode 8 (kfac_factor_channel_x3): CHANNEL factors with 8 < n <= 32, bf16x3 from HBM
-  if (o.layout == KFAC_CHANNEL && !o.has_ones && n > 8 && n <= 32 && knobs().conv_x3) {
+  if (o.layout == KFAC_CHANNEL && n > 8 && n <= 32 && knobs().conv_x3) {
     g.mode = 8;
     g.units = 1;
   }

@@ -226,7 +226,7 @@ def test_channel_x3(hip_device, B, cout, hw):
 @pytest.mark.parametrize("cout", [6, 16])
 def test_channel_operand_with_ones(hip_device, cout):
     """A CHANNEL operand with a ones column (legal in the C ABI, unused by the hooks):
-    F = [G | 1]^T [G | 1] stays on the staged kernel, which has the ones plane."""
+    F = [G | 1]^T [G | 1] on the unstaged kernel (the channel kernels have no ones row)."""
     from bnn_kfac_amd import _native as N
     B, L = 64, 36
     rng = np.random.default_rng(cout)
@@ -238,7 +238,10 @@ def test_channel_operand_with_ones(hip_device, cout):
     N.factor_update([N.factor_job(op, F, 1.0, 0.0)], hip_device)
     torch.cuda.synchronize()
     X = np.concatenate([g.transpose(0, 2, 1).reshape(-1, cout), np.ones((B * L, 1), np.float32)], 1)
-    np.testing.assert_allclose(F.cpu().numpy(), X.T.astype(np.float64) @ X, **FT)
+    W = X.T.astype(np.float64) @ X
+    # (fp32 sums of 2,304 products on the fp32 kernel: entries near zero carry the
+    # rounding of the whole sum, so the absolute bound is relative to max |W|)
+    np.testing.assert_allclose(F.cpu().numpy(), W, rtol=1e-5, atol=1e-6 * np.abs(W).max())
 
 
 @pytest.mark.gpu
