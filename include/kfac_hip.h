@@ -329,7 +329,7 @@ KFAC_API int kfac_tri_unpack(const kfac_tri_job* jobs, int njobs, const float* p
  *   0 kfac_factor_tiles_t (fp32-MFMA SYRK: row-major, LDS-DMA, register-staged conv),
  *   1 kfac_factor_reduce, 2 the whole invert call, 3 kfac_quad tiles,
  *   4 kfac_factor_syrk3 (bf16x3, split in the workgroup; largest n >= 2048),
- *   5 kfac_factor_tiles_x3 (bf16x3, split in registers; largest n >= 512),
+ *   5 kfac_factor_tiles_x3 (bf16x3, split in registers; largest n >= 256),
  *   6 kfac_factor_conv (image-staged conv factors, both the im2col and the
  *     channel-major operand), 7 kfac_factor_channel_small (channel factors n <= 8),
  *   8 the whole kfac_syev call,
@@ -337,7 +337,9 @@ KFAC_API int kfac_tri_unpack(const kfac_tri_job* jobs, int njobs, const float* p
  *   10 kfac_factor_conv_x3s (im2col factors with 17 <= n <= 32, bf16x3 from
  *     column-shifted image copies),
  *   11 kfac_factor_conv_x3f (stride-1 im2col factors with 32 < n <= 160, bf16x3 from
- *     flattened column copies).
+ *     flattened column copies),
+ *   12 kfac_factor_channel_x3 (channel-major factors with 8 < n <= 32, bf16x3 from
+ *     fragments loaded straight from HBM).
  * kfac_profile_read syncs the recorded events.  kfac_profile_read_work also
  * returns the slot's algorithmic work: `work` = flops, for the factor slots (0, 4-7, 9-12)
  * sum_jobs K_rows * n (n + 1) (lower triangle incl. the diagonal, 2 flops per
